@@ -1,0 +1,192 @@
+/*
+ * rs_mi355x.h -- C ABI of the MI355X (gfx950) Reed-Solomon GF(2^16) engine.
+ *
+ * Drop-in boundary for AndersTrier/reed-solomon-simd v3.1.0 (reference mounted
+ * at /root/reference; paths below are relative to it).  Plain pointers and
+ * sizes only; device pointers are HIP device allocations, `stream` is a
+ * hipStream_t passed as void* (NULL = default stream).
+ *
+ *   reference item                                   replaced by
+ *   -----------------------------------------------  ------------------------------
+ *   Error enum + fields        src/lib.rs:48-142     rs_status / rs_error
+ *   encode()/decode()          src/lib.rs:251-353    rs_encode / rs_decode (host buffers)
+ *   ReedSolomonEncoder         src/reed_solomon.rs:13-81
+ *     ::new / ::reset / ::supports                    rs_encoder_new / _reset / rs_supports
+ *     ::add_original_shard                            rs_encoder_add_original_shard
+ *     ::encode -> EncoderResult                       rs_encoder_encode
+ *     EncoderResult::recovery  src/encoder_result.rs:17-33   rs_encoder_recovery
+ *     EncoderResult Drop (reset_received)             rs_encoder_result_drop
+ *   ReedSolomonDecoder         src/reed_solomon.rs:83-183
+ *     ::add_original_shard / ::add_recovery_shard     rs_decoder_add_*_shard
+ *     ::decode -> DecoderResult                       rs_decoder_decode
+ *     DecoderResult::restored_original src/decoder_result.rs:17-33  rs_decoder_restored_original
+ *   DefaultRate / HighRate / LowRate  src/rate/rate_*.rs  rs_rate (RS_RATE_DEFAULT/HIGH/LOW)
+ *   trait Engine               src/engine.rs:234-291
+ *     fft / ifft (ShardsRefMut, pos, size, trunc, skew_delta)  rs_engine_fft / rs_engine_ifft
+ *     mul(x, log_m)                                   rs_engine_mul
+ *     eval_poly(erasures, truncated)                  rs_engine_eval_poly (host array)
+ *   tables::get_exp_log / get_skew  src/engine/tables.rs:98-165  rs_table_exp/log/skew
+ *
+ * Device-resident batch entry points (the performance path; no reference
+ * counterpart because the reference engine only sees host slices):
+ *   rs_encode_device / rs_decode_device
+ *
+ * Thread-safety: a context may be shared by threads (like DefaultEngine:
+ * Send + Sync, src/lib.rs:385-409); an encoder/decoder handle is used by one
+ * thread at a time (like &mut ReedSolomonEncoder).
+ */
+#ifndef RS_MI355X_H
+#define RS_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error codes, one per reference Error variant (src/lib.rs:48-142). */
+typedef enum rs_status {
+    RS_OK = 0,
+    RS_ERR_DIFFERENT_SHARD_SIZE = 1,            /* shard_bytes, got */
+    RS_ERR_DUPLICATE_ORIGINAL_SHARD_INDEX = 2,  /* index */
+    RS_ERR_DUPLICATE_RECOVERY_SHARD_INDEX = 3,  /* index */
+    RS_ERR_INVALID_ORIGINAL_SHARD_INDEX = 4,    /* original_count, index */
+    RS_ERR_INVALID_RECOVERY_SHARD_INDEX = 5,    /* recovery_count, index */
+    RS_ERR_INVALID_SHARD_SIZE = 6,              /* shard_bytes */
+    RS_ERR_NOT_ENOUGH_SHARDS = 7,               /* original_count, original_received_count, recovery_received_count */
+    RS_ERR_TOO_FEW_ORIGINAL_SHARDS = 8,         /* original_count, original_received_count */
+    RS_ERR_TOO_MANY_ORIGINAL_SHARDS = 9,        /* original_count */
+    RS_ERR_UNSUPPORTED_SHARD_COUNT = 10,        /* original_count, recovery_count */
+    /* not in the reference: */
+    RS_ERR_DEVICE = 100,                        /* HIP runtime failure (message via rs_last_device_error) */
+    RS_ERR_INVALID_ARGUMENT = 101               /* null handle / pointer, or unsupported device-API layout */
+} rs_status;
+
+/* Error payload; fields not used by a variant are 0.  Field names follow the
+ * reference variants' fields. */
+typedef struct rs_error {
+    int32_t code; /* rs_status */
+    uint64_t original_count;
+    uint64_t recovery_count;
+    uint64_t shard_bytes;
+    uint64_t got;
+    uint64_t index;
+    uint64_t original_received_count;
+    uint64_t recovery_received_count;
+} rs_error;
+
+typedef enum rs_rate { RS_RATE_DEFAULT = 0, RS_RATE_HIGH = 1, RS_RATE_LOW = 2 } rs_rate;
+
+typedef struct rs_context rs_context;
+typedef struct rs_encoder rs_encoder;
+typedef struct rs_decoder rs_decoder;
+
+/* ---- context: one per device; builds and uploads the GF tables once ---- */
+rs_status rs_context_create(int device, rs_context **out);
+void rs_context_destroy(rs_context *ctx);
+const char *rs_last_device_error(void);
+const char *rs_version(void);
+
+/* ---- capability / validation (src/rate/rate_default.rs:15-64, src/rate.rs:91-106) ---- */
+int rs_supports(rs_rate rate, uint64_t original_count, uint64_t recovery_count);
+/* 1 = HighRate, 0 = LowRate, -1 = unsupported */
+int rs_use_high_rate(uint64_t original_count, uint64_t recovery_count);
+rs_status rs_validate(rs_rate rate, uint64_t original_count, uint64_t recovery_count, uint64_t shard_bytes,
+                      rs_error *err);
+/* work_count of the encoder / decoder (rate_high.rs:135-141, 308-312; rate_low.rs same) */
+uint64_t rs_encoder_work_count(rs_rate rate, uint64_t original_count, uint64_t recovery_count);
+uint64_t rs_decoder_work_count(rs_rate rate, uint64_t original_count, uint64_t recovery_count);
+
+/* ---- one-shot host API (src/lib.rs:251-353) ----
+ * rs_encode: `original` = array of original_count pointers to shard_bytes each;
+ *   recovery_out = recovery_count * shard_bytes contiguous.
+ * rs_decode: original/recovery = arrays of (index, pointer) given as parallel
+ *   arrays; restored_out = original_count * shard_bytes, only missing rows
+ *   written; restored_mask (original_count bytes) set to 1 for restored rows. */
+rs_status rs_encode(rs_context *ctx, uint64_t original_count, uint64_t recovery_count, uint64_t shard_bytes,
+                    const uint8_t *const *original, uint64_t original_given, uint8_t *recovery_out, rs_error *err);
+rs_status rs_decode(rs_context *ctx, uint64_t original_count, uint64_t recovery_count, uint64_t shard_bytes,
+                    const uint64_t *original_index, const uint8_t *const *original, uint64_t original_given,
+                    const uint64_t *recovery_index, const uint8_t *const *recovery, uint64_t recovery_given,
+                    uint8_t *restored_out, uint8_t *restored_mask, rs_error *err);
+
+/* ---- ReedSolomonEncoder / RateEncoder (src/reed_solomon.rs, src/rate.rs:113-173) ---- */
+rs_status rs_encoder_new(rs_context *ctx, rs_rate rate, uint64_t original_count, uint64_t recovery_count,
+                         uint64_t shard_bytes, rs_encoder **out, rs_error *err);
+rs_status rs_encoder_reset(rs_encoder *enc, uint64_t original_count, uint64_t recovery_count,
+                           uint64_t shard_bytes, rs_error *err);
+rs_status rs_encoder_add_original_shard(rs_encoder *enc, const uint8_t *shard, uint64_t len, rs_error *err);
+rs_status rs_encoder_encode(rs_encoder *enc, rs_error *err);
+/* valid after a successful encode until rs_encoder_result_drop / next mutation;
+ * NULL when index >= recovery_count (src/rate/encoder_work.rs:90-96) */
+const uint8_t *rs_encoder_recovery(rs_encoder *enc, uint64_t index);
+void rs_encoder_result_drop(rs_encoder *enc); /* EncoderResult::drop -> reset_received */
+int rs_encoder_is_high_rate(const rs_encoder *enc);
+void rs_encoder_free(rs_encoder *enc);
+
+/* ---- ReedSolomonDecoder / RateDecoder (src/reed_solomon.rs, src/rate.rs:179-250) ---- */
+rs_status rs_decoder_new(rs_context *ctx, rs_rate rate, uint64_t original_count, uint64_t recovery_count,
+                         uint64_t shard_bytes, rs_decoder **out, rs_error *err);
+rs_status rs_decoder_reset(rs_decoder *dec, uint64_t original_count, uint64_t recovery_count,
+                           uint64_t shard_bytes, rs_error *err);
+rs_status rs_decoder_add_original_shard(rs_decoder *dec, uint64_t index, const uint8_t *shard, uint64_t len,
+                                        rs_error *err);
+rs_status rs_decoder_add_recovery_shard(rs_decoder *dec, uint64_t index, const uint8_t *shard, uint64_t len,
+                                        rs_error *err);
+rs_status rs_decoder_decode(rs_decoder *dec, rs_error *err);
+/* NULL unless original `index` was missing and has been restored
+ * (src/rate/decoder_work.rs:189-197) */
+const uint8_t *rs_decoder_restored_original(rs_decoder *dec, uint64_t index);
+uint64_t rs_decoder_restored_count(const rs_decoder *dec);
+void rs_decoder_result_drop(rs_decoder *dec); /* DecoderResult::drop -> reset_received */
+int rs_decoder_is_high_rate(const rs_decoder *dec);
+void rs_decoder_free(rs_decoder *dec);
+
+/* ---- device-resident batch path (HBM in, HBM out) ----
+ * d_original: original_count rows, d_recovery: recovery_count rows, both
+ * row-major with row stride shard_bytes.  shard_bytes must be a positive
+ * multiple of 64 (the reference's native block layout, algorithm.md:18-31;
+ * other even sizes go through the host API, which re-packs the tail block).
+ * Asynchronous on `stream`; scratch is owned by the context (one call in
+ * flight per context per stream). */
+rs_status rs_encode_device(rs_context *ctx, rs_rate rate, uint64_t original_count, uint64_t recovery_count,
+                           uint64_t shard_bytes, const void *d_original, void *d_recovery, void *stream,
+                           rs_error *err);
+/* original_present / recovery_present: HOST arrays of 0/1 bytes.
+ * d_restored: original_count rows; only missing originals are written.
+ * Missing rows of d_original / d_recovery are never read. */
+rs_status rs_decode_device(rs_context *ctx, rs_rate rate, uint64_t original_count, uint64_t recovery_count,
+                           uint64_t shard_bytes, const void *d_original, const uint8_t *original_present,
+                           const void *d_recovery, const uint8_t *recovery_present, void *d_restored, void *stream,
+                           rs_error *err);
+
+/* ---- Engine trait over a device shard matrix (src/engine.rs:234-291) ----
+ * d_rows: shard_count rows of shard_len_64 64-byte blocks (ShardsRefMut,
+ * src/engine/shards.rs:100-189).  Infallible in the reference (debug_assert on
+ * bad args); here bad args return RS_ERR_INVALID_ARGUMENT. */
+rs_status rs_engine_fft(rs_context *ctx, void *d_rows, uint64_t shard_count, uint64_t shard_len_64, uint64_t pos,
+                        uint64_t size, uint64_t truncated_size, uint64_t skew_delta, void *stream);
+rs_status rs_engine_ifft(rs_context *ctx, void *d_rows, uint64_t shard_count, uint64_t shard_len_64, uint64_t pos,
+                         uint64_t size, uint64_t truncated_size, uint64_t skew_delta, void *stream);
+rs_status rs_engine_mul(rs_context *ctx, void *d_rows, uint64_t block_count, uint16_t log_m, void *stream);
+/* host array of 65536 elements, in place (src/engine/utils.rs:20-31) */
+void rs_engine_eval_poly(uint16_t *erasures, uint64_t truncated_size);
+/* formal derivative over all shard_count rows (src/engine/utils.rs:99-104) */
+rs_status rs_engine_formal_derivative(rs_context *ctx, void *d_rows, uint64_t shard_count, uint64_t shard_len_64,
+                                      void *stream);
+
+/* ---- GF(2^16) tables (src/engine/tables.rs), host copies ---- */
+const uint16_t *rs_table_exp(void);       /* 65536 */
+const uint16_t *rs_table_log(void);       /* 65536 */
+const uint16_t *rs_table_skew(void);      /* 65535 */
+const uint16_t *rs_table_log_walsh(void); /* 65536 */
+/* this engine's byte-permute multiply tables, 20 words per entry, 65536
+ * entries (format: reed-solomon-simd_amd/csrc/gf_tables.cpp fill_perm) */
+const uint32_t *rs_table_perm_by_log(void);
+const uint32_t *rs_table_perm_by_skew(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -264,6 +264,20 @@ static void extract_shard(const uint8_t *work, size_t blocks, size_t row, uint8_
     }
 }
 
+/* Work buffer re-used across calls, like the reference's EncoderWork /
+ * DecoderWork (shards.rs:30-36 keeps its allocation). */
+static uint8_t *g_work = NULL;
+static size_t g_work_cap = 0;
+static uint8_t *work_buf(size_t bytes) {
+    if (bytes > g_work_cap) {
+        free(g_work);
+        g_work = malloc(bytes);
+        g_work_cap = bytes;
+    }
+    memset(g_work, 0, bytes);
+    return g_work;
+}
+
 static size_t next_pow2(size_t x) { size_t p = 1; while (p < x) p <<= 1; return p; }
 static size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 
@@ -311,7 +325,7 @@ int orc_encode(int rate, size_t N, size_t M, size_t S, const uint8_t *orig, uint
     size_t blocks = (S + 63) / 64;
     if (high) {
         size_t n = next_pow2(M), rows = round_up(N, n);
-        uint8_t *w = calloc(rows * blocks, 64);
+        uint8_t *w = work_buf(rows * blocks * 64);
         for (size_t i = 0; i < N; i++) insert_shard(w, blocks, i, orig + i * S, S);
         /* rate_high.rs:44-87: chunk c transformed with skew_delta = c*n + n,
          * all chunks XOR-folded into chunk 0, then one FFT with skew_delta 0. */
@@ -324,10 +338,9 @@ int orc_encode(int rate, size_t N, size_t M, size_t S, const uint8_t *orig, uint
         }
         E_fft(w, blocks, 0, n, M, 0);
         for (size_t i = 0; i < M; i++) extract_shard(w, blocks, i, rec + i * S, S);
-        free(w);
     } else {
         size_t n = next_pow2(N), rows = round_up(M, n);
-        uint8_t *w = calloc(rows * blocks, 64);
+        uint8_t *w = work_buf(rows * blocks * 64);
         for (size_t i = 0; i < N; i++) insert_shard(w, blocks, i, orig + i * S, S);
         /* rate_low.rs:44-87: one IFFT (skew 0), replicated into every output
          * chunk, chunk c transformed with FFT skew_delta = c*n + n. */
@@ -338,7 +351,6 @@ int orc_encode(int rate, size_t N, size_t M, size_t S, const uint8_t *orig, uint
             E_fft(w, blocks, c0, n, cnt, c0 + n);
         }
         for (size_t i = 0; i < M; i++) extract_shard(w, blocks, i, rec + i * S, S);
-        free(w);
     }
     return E_OK;
 }
@@ -361,7 +373,7 @@ int orc_decode(int rate, size_t N, size_t M, size_t S, const uint8_t *orig, cons
     size_t chunk = high ? next_pow2(M) : next_pow2(N);
     size_t rec_base = high ? 0 : chunk, orig_base = high ? chunk : 0;
     size_t rows = next_pow2(chunk + (high ? N : M));
-    uint8_t *w = calloc(rows * blocks, 64);
+    uint8_t *w = work_buf(rows * blocks * 64);
     uint8_t *got = calloc(rows, 1);
     for (size_t i = 0; i < N; i++)
         if (orig_present[i]) { insert_shard(w, blocks, orig_base + i, orig + i * S, S); got[orig_base + i] = 1; }
@@ -399,7 +411,7 @@ int orc_decode(int rate, size_t N, size_t M, size_t S, const uint8_t *orig, cons
             extract_shard(w, blocks, p, restored + i * S, S);
         }
     }
-    free(w); free(got); free(er);
+    free(got); free(er);
     return E_OK;
 }
 

@@ -1,0 +1,860 @@
+// Host side of the MI355X Reed-Solomon engine: GF tables on the device, the
+// HighRate / LowRate orchestration as device passes, the encoder / decoder
+// objects and the extern "C" boundary declared in include/rs_mi355x.h.
+//
+// Rate semantics follow reference src/rate/rate_high.rs:44-254,
+// src/rate/rate_low.rs:44-254, src/rate/rate_default.rs:15-64; validation and
+// error order follow src/rate.rs:91-106, src/rate/encoder_work.rs:50-87,
+// src/rate/decoder_work.rs:62-141, src/lib.rs:251-353.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rs_mi355x.h"
+#include "gf_tables.hpp"
+#include "rs_device.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+uint64_t next_pow2(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+uint32_t ilog2(uint64_t x) {
+    uint32_t l = 0;
+    while ((uint64_t(1) << l) < x) ++l;
+    return l;
+}
+uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
+
+struct DevError {
+    hipError_t e;
+};
+void check(hipError_t e) {
+    if (e != hipSuccess) throw DevError{e};
+}
+
+rs_status set_err(rs_error *err, rs_status code) {
+    if (err) {
+        std::memset(err, 0, sizeof *err);
+        err->code = code;
+    }
+    return code;
+}
+
+// ---------------------------------------------------------------------------
+// rate selection (rate_default.rs:15-64, rate_high.rs:19-25, rate_low.rs:19-25)
+
+bool high_supported(uint64_t N, uint64_t M) {
+    return N > 0 && M > 0 && N < 65536 && M < 65536 && next_pow2(M) + N <= 65536;
+}
+bool low_supported(uint64_t N, uint64_t M) {
+    return N > 0 && M > 0 && N < 65536 && M < 65536 && next_pow2(N) + M <= 65536;
+}
+int use_high_rate(uint64_t N, uint64_t M) {
+    if (N > 65536 || M > 65536 || N == 0 || M == 0) return -1;
+    const uint64_t pn = next_pow2(N), pm = next_pow2(M);
+    if (std::min(pn, pm) + std::max(N, M) > 65536) return -1;
+    if (pn != pm) return pn > pm ? 1 : 0;
+    return N <= M ? 1 : 0;
+}
+
+// resolves `rate` for (N, M, S) with the reference's error order; returns
+// 1 = high, 0 = low, or sets err and returns -1
+int resolve(rs_rate rate, uint64_t N, uint64_t M, uint64_t S, rs_error *err) {
+    int high;
+    if (rate == RS_RATE_HIGH) high = 1;
+    else if (rate == RS_RATE_LOW) high = 0;
+    else high = use_high_rate(N, M);
+    if (high < 0 || (high ? !high_supported(N, M) : !low_supported(N, M))) {
+        set_err(err, RS_ERR_UNSUPPORTED_SHARD_COUNT);
+        if (err) err->original_count = N, err->recovery_count = M;
+        return -1;
+    }
+    if (S == 0 || (S & 1)) {
+        set_err(err, RS_ERR_INVALID_SHARD_SIZE);
+        if (err) err->shard_bytes = S;
+        return -1;
+    }
+    return high;
+}
+
+// Device-side scratch that grows monotonically.
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    void *get(size_t bytes) {
+        if (bytes > cap) {
+            if (p) check(hipFree(p));
+            p = nullptr;
+            check(hipMalloc(&p, bytes));
+            cap = bytes;
+        }
+        return p;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+struct Workspace {
+    DevBuf work, work2, rowinfo, state;
+    std::vector<uint8_t> h_state;
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+struct rs_context {
+    int device = 0;
+    uint32_t *d_tw = nullptr;
+    uint32_t *d_lut = nullptr;
+    uint16_t *d_lwfold = nullptr;
+    uint16_t lw0 = 0;
+    std::mutex mu;  // guards ws (device-resident API scratch)
+    Workspace ws;
+};
+
+namespace {
+
+// Geometry of a device shard matrix: rows of `stride` bytes, `packs` packs of
+// 4 elements each (8 bytes: 4 low + 4 high) per row.
+struct Geom {
+    uint64_t stride;
+    uint32_t packs;
+};
+
+rs::PassArgs base_args(rs_context *ctx, const Geom &g, uint32_t n) {
+    rs::PassArgs A;
+    A.n = n;
+    A.packs = g.packs;
+    A.slices = (g.packs + 63) / 64;
+    A.tw = ctx->d_tw;
+    A.lut = ctx->d_lut;
+    return A;
+}
+
+// split of a 2^L transform into passes: L <= 8 -> single; else low bits [0,a)
+// in passes A/C, high bits [a, L) in the fused pass B.
+struct Split {
+    bool single;
+    uint32_t L, a, kb;
+};
+Split split(uint32_t L) {
+    if (L <= 8) return {true, L, 0, L};
+    const uint32_t a = (L + 1) / 2;
+    return {false, L, a, L - a};
+}
+
+void launch(int K, int flags, rs::PassArgs A, uint32_t nsets, uint32_t a, hipStream_t s) {
+    A.nsets = nsets;
+    A.a = a;
+    check(rs::launch_pass(K, flags, A, s));
+}
+
+// HighRate encode (rate_high.rs:44-87) from device rows to device rows.
+void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint64_t M, const uint8_t *orig,
+                 uint8_t *rec, hipStream_t s) {
+    const uint32_t n = uint32_t(next_pow2(M)), L = ilog2(n);
+    const uint32_t C = uint32_t((N + n - 1) / n);
+    const Split sp = split(L);
+    rs::PassArgs A = base_args(ctx, g, n);
+    A.ifft_delta = n;
+    A.ifft_delta_step = n;
+    if (sp.single) {
+        A.src[0] = {orig, g.stride, 0, uint32_t(N)};
+        A.nsrc = 1;
+        A.in_chunks = C;
+        A.dst = {rec, g.stride, 0, uint32_t(M)};
+        launch(L, rs::kIfft | rs::kFft, A, 1, 0, s);
+        return;
+    }
+    uint8_t *W = static_cast<uint8_t *>(ws.work.get(size_t(C) * n * g.stride));
+    rs::PassArgs P1 = A;  // IFFT low bits, per chunk
+    P1.src[0] = {orig, g.stride, 0, uint32_t(N)};
+    P1.nsrc = 1;
+    P1.grid_chunks = C;
+    P1.work_out = W;
+    P1.work_stride = g.stride;
+    launch(sp.a, rs::kIfft, P1, n >> sp.a, 0, s);
+    rs::PassArgs P2 = A;  // IFFT high bits per chunk, XOR-fold, FFT high bits
+    P2.work_in = W;
+    P2.work_stride = g.stride;
+    P2.in_chunks = C;
+    P2.work_out = W;
+    launch(sp.kb, rs::kIfft | rs::kFft, P2, 1u << sp.a, sp.a, s);
+    rs::PassArgs P3 = A;  // FFT low bits -> recovery rows
+    P3.work_in = W;
+    P3.work_stride = g.stride;
+    P3.dst = {rec, g.stride, 0, uint32_t(M)};
+    launch(sp.a, rs::kFft, P3, n >> sp.a, 0, s);
+}
+
+// LowRate encode (rate_low.rs:44-87).
+void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint64_t M, const uint8_t *orig,
+                uint8_t *rec, hipStream_t s) {
+    const uint32_t n = uint32_t(next_pow2(N)), L = ilog2(n);
+    const uint32_t C = uint32_t((M + n - 1) / n);
+    const Split sp = split(L);
+    rs::PassArgs A = base_args(ctx, g, n);
+    A.fft_delta = n;
+    A.fft_delta_step = n;
+    if (sp.single) {
+        A.src[0] = {orig, g.stride, 0, uint32_t(N)};
+        A.nsrc = 1;
+        A.out_chunks = C;
+        A.dst = {rec, g.stride, 0, uint32_t(M)};
+        launch(L, rs::kIfft | rs::kFft, A, 1, 0, s);
+        return;
+    }
+    uint8_t *W = static_cast<uint8_t *>(ws.work.get(size_t(n) * g.stride));
+    uint8_t *W2 = static_cast<uint8_t *>(ws.work2.get(size_t(C) * n * g.stride));
+    rs::PassArgs P1 = A;
+    P1.src[0] = {orig, g.stride, 0, uint32_t(N)};
+    P1.nsrc = 1;
+    P1.work_out = W;
+    P1.work_stride = g.stride;
+    launch(sp.a, rs::kIfft, P1, n >> sp.a, 0, s);
+    rs::PassArgs P2 = A;
+    P2.work_in = W;
+    P2.work_stride = g.stride;
+    P2.out_chunks = C;
+    P2.work_out = W2;
+    launch(sp.kb, rs::kIfft | rs::kFft, P2, 1u << sp.a, sp.a, s);
+    rs::PassArgs P3 = A;
+    P3.work_in = W2;
+    P3.work_stride = g.stride;
+    P3.grid_chunks = C;
+    P3.dst = {rec, g.stride, 0, uint32_t(M)};
+    launch(sp.a, rs::kFft, P3, n >> sp.a, 0, s);
+}
+
+// Decode (rate_high.rs:172-254 / rate_low.rs:172-254).  Only missing original
+// rows of `restored` are written.
+void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64_t N, uint64_t M,
+                const uint8_t *orig, const uint8_t *orig_present, const uint8_t *rec, const uint8_t *rec_present,
+                uint8_t *restored, hipStream_t s) {
+    const uint32_t chunk = uint32_t(high ? next_pow2(M) : next_pow2(N));
+    const uint32_t end = uint32_t(chunk + (high ? N : M));
+    const uint32_t nd = uint32_t(next_pow2(end)), u = ilog2(nd);
+    // erasure vector + received flags per work row
+    std::vector<uint8_t> &st = ws.h_state;
+    st.assign(nd, 0);
+    if (high) {
+        for (uint32_t r = 0; r < M; ++r) st[r] = rec_present[r] ? 2 : 1;
+        for (uint32_t r = uint32_t(M); r < chunk; ++r) st[r] = 1;
+        for (uint32_t r = chunk; r < end; ++r) st[r] = orig_present[r - chunk] ? 2 : 1;
+    } else {
+        for (uint32_t r = 0; r < N; ++r) st[r] = orig_present[r] ? 2 : 1;
+        for (uint32_t r = chunk; r < end; ++r) st[r] = rec_present[r - chunk] ? 2 : 1;
+    }
+    uint8_t *d_state = static_cast<uint8_t *>(ws.state.get(nd));
+    uint32_t *d_rowinfo = static_cast<uint32_t *>(ws.rowinfo.get(size_t(nd) * 4));
+    check(hipMemcpyAsync(d_state, st.data(), nd, hipMemcpyHostToDevice, s));
+    check(rs::launch_eval_poly(u, !high, end, d_state, ctx->d_lwfold + (nd - 1), ctx->lw0, d_rowinfo, s));
+
+    rs::PassArgs A = base_args(ctx, g, nd);
+    A.rowinfo = d_rowinfo;
+    const rs::RowMap rec_map{rec, g.stride, high ? 0u : chunk, high ? uint32_t(M) : end};
+    const rs::RowMap orig_map{orig, g.stride, high ? chunk : 0u, high ? end : uint32_t(N)};
+    const rs::RowMap out_map{restored, g.stride, orig_map.row_begin, orig_map.row_end};
+    const Split sp = split(u);
+    if (sp.single) {
+        A.src[0] = rec_map;
+        A.src[1] = orig_map;
+        A.nsrc = 2;
+        A.load_scale = 1;
+        A.fd_mode = 2;
+        A.dst = out_map;
+        A.reveal = 1;
+        launch(u, rs::kIfft | rs::kFft, A, 1, 0, s);
+        return;
+    }
+    uint8_t *W = static_cast<uint8_t *>(ws.work.get(size_t(nd) * g.stride));
+    uint8_t *Z = static_cast<uint8_t *>(ws.work2.get(size_t(nd) * g.stride));
+    rs::PassArgs P1 = A;  // scale received rows, IFFT low bits -> W
+    P1.src[0] = rec_map;
+    P1.src[1] = orig_map;
+    P1.nsrc = 2;
+    P1.load_scale = 1;
+    P1.work_out = W;
+    P1.work_stride = g.stride;
+    launch(sp.a, rs::kIfft, P1, nd >> sp.a, 0, s);
+    rs::PassArgs P2 = A;  // IFFT high, H-part of the derivative, FFT high -> Z
+    P2.work_in = W;
+    P2.work_stride = g.stride;
+    P2.fd_mode = 1;
+    P2.work_out = Z;
+    launch(sp.kb, rs::kIfft | rs::kFft, P2, 1u << sp.a, sp.a, s);
+    rs::PassArgs P3 = A;  // (I + Lo) W ^ Z, FFT low, reveal missing originals
+    P3.work_in = W;
+    P3.work_stride = g.stride;
+    P3.fd_mode = 2;
+    P3.xor_in = Z;
+    P3.dst = out_map;
+    P3.reveal = 1;
+    launch(sp.a, rs::kFft, P3, nd >> sp.a, 0, s);
+}
+
+const char *hip_msg(hipError_t e) { return hipGetErrorString(e); }
+
+}  // namespace
+
+// ===========================================================================
+// encoder / decoder objects
+
+struct rs_encoder {
+    rs_context *ctx;
+    rs_rate rate;
+    bool high = true;
+    uint64_t N = 0, M = 0, S = 0, row = 0, received = 0;
+    bool has_result = false;
+    std::vector<uint8_t> h_orig, h_rec;  // padded rows / unpadded result
+    DevBuf d_orig, d_rec;
+    Workspace ws;
+};
+
+struct rs_decoder {
+    rs_context *ctx;
+    rs_rate rate;
+    bool high = true;
+    uint64_t N = 0, M = 0, S = 0, row = 0;
+    uint64_t orig_received = 0, rec_received = 0;
+    bool has_result = false, decoded = false;
+    std::vector<uint8_t> orig_present, rec_present;
+    std::vector<uint8_t> h_orig, h_rec, h_out;
+    DevBuf d_orig, d_rec, d_out;
+    Workspace ws;
+};
+
+namespace {
+
+// tail re-pack of a shard into padded 64-byte blocks (shards.rs:38-59)
+void insert_row(uint8_t *dst, const uint8_t *src, uint64_t S) {
+    const uint64_t whole = S / 64, tail = S % 64;
+    std::memcpy(dst, src, whole * 64);
+    if (tail) {
+        uint8_t *blk = dst + whole * 64;
+        std::memset(blk, 0, 64);
+        std::memcpy(blk, src + whole * 64, tail / 2);
+        std::memcpy(blk + 32, src + whole * 64 + tail / 2, tail / 2);
+    }
+}
+// undo (shards.rs:62-74)
+void extract_row(uint8_t *dst, const uint8_t *src, uint64_t S) {
+    const uint64_t whole = S / 64, tail = S % 64;
+    std::memcpy(dst, src, whole * 64);
+    if (tail) {
+        std::memcpy(dst + whole * 64, src + whole * 64, tail / 2);
+        std::memcpy(dst + whole * 64 + tail / 2, src + whole * 64 + 32, tail / 2);
+    }
+}
+
+template <typename F>
+rs_status guarded(rs_error *err, F &&f) {
+    try {
+        return f();
+    } catch (const DevError &d) {
+        g_last_error = hip_msg(d.e);
+        return set_err(err, RS_ERR_DEVICE);
+    } catch (const std::bad_alloc &) {
+        g_last_error = "host allocation failed";
+        return set_err(err, RS_ERR_DEVICE);
+    }
+}
+
+rs_status encoder_configure(rs_encoder *e, uint64_t N, uint64_t M, uint64_t S, rs_error *err) {
+    const int high = resolve(e->rate, N, M, S, err);
+    if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
+    e->high = high;
+    e->N = N, e->M = M, e->S = S;
+    e->row = round_up(S, 64);
+    e->received = 0;
+    e->has_result = false;
+    e->h_orig.resize(N * e->row);
+    return set_err(err, RS_OK);
+}
+
+rs_status decoder_configure(rs_decoder *d, uint64_t N, uint64_t M, uint64_t S, rs_error *err) {
+    const int high = resolve(d->rate, N, M, S, err);
+    if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
+    d->high = high;
+    d->N = N, d->M = M, d->S = S;
+    d->row = round_up(S, 64);
+    d->orig_received = d->rec_received = 0;
+    d->has_result = d->decoded = false;
+    d->orig_present.assign(N, 0);
+    d->rec_present.assign(M, 0);
+    d->h_orig.resize(N * d->row);
+    d->h_rec.resize(M * d->row);
+    return set_err(err, RS_OK);
+}
+
+void encoder_drop_result(rs_encoder *e) {
+    if (e->has_result) {
+        e->has_result = false;
+        e->received = 0;  // EncoderResult::drop -> reset_received (encoder_result.rs:48-52)
+    }
+}
+void decoder_drop_result(rs_decoder *d) {
+    if (d->has_result) {
+        d->has_result = d->decoded = false;  // DecoderResult::drop (decoder_result.rs:44-48)
+        d->orig_received = d->rec_received = 0;
+        std::fill(d->orig_present.begin(), d->orig_present.end(), 0);
+        std::fill(d->rec_present.begin(), d->rec_present.end(), 0);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *rs_last_device_error(void) { return g_last_error.c_str(); }
+const char *rs_version(void) { return "rs-mi355x 0.1.0 (gfx950)"; }
+
+rs_status rs_context_create(int device, rs_context **out) {
+    if (!out) return RS_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    auto *ctx = new rs_context;
+    ctx->device = device;
+    rs_status st = guarded(nullptr, [&]() -> rs_status {
+        check(hipSetDevice(device));
+        const rs::GfTables &T = rs::tables();
+        check(hipMalloc(&ctx->d_tw, T.perm_by_skew.size() * 4));
+        check(hipMalloc(&ctx->d_lut, T.perm_by_log.size() * 4));
+        check(hipMalloc(&ctx->d_lwfold, T.lw_fold.size() * 2));
+        check(hipMemcpy(ctx->d_tw, T.perm_by_skew.data(), T.perm_by_skew.size() * 4, hipMemcpyHostToDevice));
+        check(hipMemcpy(ctx->d_lut, T.perm_by_log.data(), T.perm_by_log.size() * 4, hipMemcpyHostToDevice));
+        check(hipMemcpy(ctx->d_lwfold, T.lw_fold.data(), T.lw_fold.size() * 2, hipMemcpyHostToDevice));
+        ctx->lw0 = T.log_walsh[0];
+        return RS_OK;
+    });
+    if (st != RS_OK) {
+        rs_context_destroy(ctx);
+        return st;
+    }
+    *out = ctx;
+    return RS_OK;
+}
+
+void rs_context_destroy(rs_context *ctx) {
+    if (!ctx) return;
+    if (ctx->d_tw) (void)hipFree(ctx->d_tw);
+    if (ctx->d_lut) (void)hipFree(ctx->d_lut);
+    if (ctx->d_lwfold) (void)hipFree(ctx->d_lwfold);
+    delete ctx;
+}
+
+int rs_use_high_rate(uint64_t N, uint64_t M) { return use_high_rate(N, M); }
+
+int rs_supports(rs_rate rate, uint64_t N, uint64_t M) {
+    if (rate == RS_RATE_HIGH) return high_supported(N, M);
+    if (rate == RS_RATE_LOW) return low_supported(N, M);
+    return use_high_rate(N, M) >= 0;
+}
+
+rs_status rs_validate(rs_rate rate, uint64_t N, uint64_t M, uint64_t S, rs_error *err) {
+    if (resolve(rate, N, M, S, err) < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
+    return set_err(err, RS_OK);
+}
+
+uint64_t rs_encoder_work_count(rs_rate rate, uint64_t N, uint64_t M) {
+    const int high = rate == RS_RATE_HIGH ? 1 : rate == RS_RATE_LOW ? 0 : use_high_rate(N, M);
+    if (high < 0) return 0;
+    return high ? round_up(N, next_pow2(M)) : round_up(M, next_pow2(N));
+}
+
+uint64_t rs_decoder_work_count(rs_rate rate, uint64_t N, uint64_t M) {
+    const int high = rate == RS_RATE_HIGH ? 1 : rate == RS_RATE_LOW ? 0 : use_high_rate(N, M);
+    if (high < 0) return 0;
+    return high ? next_pow2(next_pow2(M) + N) : next_pow2(next_pow2(N) + M);
+}
+
+// ---- device-resident ------------------------------------------------------
+
+rs_status rs_encode_device(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, const void *d_orig,
+                           void *d_rec, void *stream, rs_error *err) {
+    if (!ctx || !d_orig || !d_rec) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    const int high = resolve(rate, N, M, S, err);
+    if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
+    if (S % 64) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    return guarded(err, [&]() -> rs_status {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        const Geom g{S, uint32_t(S / 8)};
+        auto s = static_cast<hipStream_t>(stream);
+        if (high)
+            encode_high(ctx, ctx->ws, g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
+        else
+            encode_low(ctx, ctx->ws, g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
+        return set_err(err, RS_OK);
+    });
+}
+
+rs_status rs_decode_device(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, const void *d_orig,
+                           const uint8_t *orig_present, const void *d_rec, const uint8_t *rec_present,
+                           void *d_restored, void *stream, rs_error *err) {
+    if (!ctx || !d_orig || !d_rec || !d_restored || !orig_present || !rec_present)
+        return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    const int high = resolve(rate, N, M, S, err);
+    if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
+    if (S % 64) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    uint64_t have_o = 0, have_r = 0;
+    for (uint64_t i = 0; i < N; ++i) have_o += orig_present[i] != 0;
+    for (uint64_t i = 0; i < M; ++i) have_r += rec_present[i] != 0;
+    if (have_o + have_r < N) {
+        set_err(err, RS_ERR_NOT_ENOUGH_SHARDS);
+        if (err) err->original_count = N, err->original_received_count = have_o, err->recovery_received_count = have_r;
+        return RS_ERR_NOT_ENOUGH_SHARDS;
+    }
+    if (have_o == N) return set_err(err, RS_OK);
+    return guarded(err, [&]() -> rs_status {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        const Geom g{S, uint32_t(S / 8)};
+        decode_dev(ctx, ctx->ws, high, g, N, M, static_cast<const uint8_t *>(d_orig), orig_present,
+                   static_cast<const uint8_t *>(d_rec), rec_present, static_cast<uint8_t *>(d_restored),
+                   static_cast<hipStream_t>(stream));
+        return set_err(err, RS_OK);
+    });
+}
+
+// ---- encoder ----------------------------------------------------------------
+
+rs_status rs_encoder_new(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, rs_encoder **out,
+                         rs_error *err) {
+    if (!ctx || !out) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    *out = nullptr;
+    auto *e = new rs_encoder;
+    e->ctx = ctx;
+    e->rate = rate;
+    const rs_status st = encoder_configure(e, N, M, S, err);
+    if (st != RS_OK) {
+        delete e;
+        return st;
+    }
+    *out = e;
+    return RS_OK;
+}
+
+rs_status rs_encoder_reset(rs_encoder *e, uint64_t N, uint64_t M, uint64_t S, rs_error *err) {
+    if (!e) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    e->has_result = false;
+    return encoder_configure(e, N, M, S, err);
+}
+
+rs_status rs_encoder_add_original_shard(rs_encoder *e, const uint8_t *shard, uint64_t len, rs_error *err) {
+    if (!e || (!shard && len)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    encoder_drop_result(e);
+    if (e->received == e->N) {  // encoder_work.rs:56-59
+        set_err(err, RS_ERR_TOO_MANY_ORIGINAL_SHARDS);
+        if (err) err->original_count = e->N;
+        return RS_ERR_TOO_MANY_ORIGINAL_SHARDS;
+    }
+    if (len != e->S) {  // encoder_work.rs:60-64
+        set_err(err, RS_ERR_DIFFERENT_SHARD_SIZE);
+        if (err) err->shard_bytes = e->S, err->got = len;
+        return RS_ERR_DIFFERENT_SHARD_SIZE;
+    }
+    insert_row(&e->h_orig[e->received * e->row], shard, e->S);
+    ++e->received;
+    return set_err(err, RS_OK);
+}
+
+rs_status rs_encoder_encode(rs_encoder *e, rs_error *err) {
+    if (!e) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    if (e->has_result) return set_err(err, RS_OK);
+    if (e->received != e->N) {  // encoder_work.rs:75-86
+        set_err(err, RS_ERR_TOO_FEW_ORIGINAL_SHARDS);
+        if (err) err->original_count = e->N, err->original_received_count = e->received;
+        return RS_ERR_TOO_FEW_ORIGINAL_SHARDS;
+    }
+    return guarded(err, [&]() -> rs_status {
+        check(hipSetDevice(e->ctx->device));
+        const Geom g{e->row, uint32_t(e->row / 8)};
+        auto *d_orig = static_cast<uint8_t *>(e->d_orig.get(e->N * e->row));
+        auto *d_rec = static_cast<uint8_t *>(e->d_rec.get(e->M * e->row));
+        check(hipMemcpy(d_orig, e->h_orig.data(), e->N * e->row, hipMemcpyHostToDevice));
+        if (e->high) encode_high(e->ctx, e->ws, g, e->N, e->M, d_orig, d_rec, nullptr);
+        else encode_low(e->ctx, e->ws, g, e->N, e->M, d_orig, d_rec, nullptr);
+        std::vector<uint8_t> padded(e->M * e->row);
+        check(hipMemcpy(padded.data(), d_rec, padded.size(), hipMemcpyDeviceToHost));
+        e->h_rec.resize(e->M * e->S);
+        for (uint64_t i = 0; i < e->M; ++i) extract_row(&e->h_rec[i * e->S], &padded[i * e->row], e->S);
+        e->has_result = true;
+        return set_err(err, RS_OK);
+    });
+}
+
+const uint8_t *rs_encoder_recovery(rs_encoder *e, uint64_t index) {
+    if (!e || !e->has_result || index >= e->M) return nullptr;
+    return &e->h_rec[index * e->S];
+}
+
+void rs_encoder_result_drop(rs_encoder *e) {
+    if (e) encoder_drop_result(e);
+}
+int rs_encoder_is_high_rate(const rs_encoder *e) { return e ? e->high : -1; }
+void rs_encoder_free(rs_encoder *e) { delete e; }
+
+// ---- decoder ----------------------------------------------------------------
+
+rs_status rs_decoder_new(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, rs_decoder **out,
+                         rs_error *err) {
+    if (!ctx || !out) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    *out = nullptr;
+    auto *d = new rs_decoder;
+    d->ctx = ctx;
+    d->rate = rate;
+    const rs_status st = decoder_configure(d, N, M, S, err);
+    if (st != RS_OK) {
+        delete d;
+        return st;
+    }
+    *out = d;
+    return RS_OK;
+}
+
+rs_status rs_decoder_reset(rs_decoder *d, uint64_t N, uint64_t M, uint64_t S, rs_error *err) {
+    if (!d) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    d->has_result = false;
+    return decoder_configure(d, N, M, S, err);
+}
+
+static rs_status dec_add(rs_decoder *d, bool orig, uint64_t index, const uint8_t *shard, uint64_t len, rs_error *err) {
+    if (!d || (!shard && len)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    decoder_drop_result(d);
+    const uint64_t count = orig ? d->N : d->M;
+    std::vector<uint8_t> &present = orig ? d->orig_present : d->rec_present;
+    if (index >= count) {  // decoder_work.rs:70-74, 99-103
+        set_err(err, orig ? RS_ERR_INVALID_ORIGINAL_SHARD_INDEX : RS_ERR_INVALID_RECOVERY_SHARD_INDEX);
+        if (err) {
+            (orig ? err->original_count : err->recovery_count) = count;
+            err->index = index;
+        }
+        return rs_status(err ? err->code : RS_ERR_INVALID_ARGUMENT);
+    }
+    if (present[index]) {  // :75-76, :104-105
+        set_err(err, orig ? RS_ERR_DUPLICATE_ORIGINAL_SHARD_INDEX : RS_ERR_DUPLICATE_RECOVERY_SHARD_INDEX);
+        if (err) err->index = index;
+        return orig ? RS_ERR_DUPLICATE_ORIGINAL_SHARD_INDEX : RS_ERR_DUPLICATE_RECOVERY_SHARD_INDEX;
+    }
+    if (len != d->S) {  // :77-81, :106-110
+        set_err(err, RS_ERR_DIFFERENT_SHARD_SIZE);
+        if (err) err->shard_bytes = d->S, err->got = len;
+        return RS_ERR_DIFFERENT_SHARD_SIZE;
+    }
+    insert_row(&(orig ? d->h_orig : d->h_rec)[index * d->row], shard, d->S);
+    present[index] = 1;
+    ++(orig ? d->orig_received : d->rec_received);
+    return set_err(err, RS_OK);
+}
+
+rs_status rs_decoder_add_original_shard(rs_decoder *d, uint64_t index, const uint8_t *shard, uint64_t len,
+                                        rs_error *err) {
+    return dec_add(d, true, index, shard, len, err);
+}
+rs_status rs_decoder_add_recovery_shard(rs_decoder *d, uint64_t index, const uint8_t *shard, uint64_t len,
+                                        rs_error *err) {
+    return dec_add(d, false, index, shard, len, err);
+}
+
+rs_status rs_decoder_decode(rs_decoder *d, rs_error *err) {
+    if (!d) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    if (d->has_result) return set_err(err, RS_OK);
+    if (d->orig_received + d->rec_received < d->N) {  // decoder_work.rs:125-130
+        set_err(err, RS_ERR_NOT_ENOUGH_SHARDS);
+        if (err)
+            err->original_count = d->N, err->original_received_count = d->orig_received,
+            err->recovery_received_count = d->rec_received;
+        return RS_ERR_NOT_ENOUGH_SHARDS;
+    }
+    if (d->orig_received == d->N) {  // nothing to restore (decoder_work.rs:131-132)
+        d->has_result = true;
+        d->decoded = false;
+        return set_err(err, RS_OK);
+    }
+    return guarded(err, [&]() -> rs_status {
+        check(hipSetDevice(d->ctx->device));
+        const Geom g{d->row, uint32_t(d->row / 8)};
+        auto *d_orig = static_cast<uint8_t *>(d->d_orig.get(d->N * d->row));
+        auto *d_rec = static_cast<uint8_t *>(d->d_rec.get(d->M * d->row));
+        auto *d_out = static_cast<uint8_t *>(d->d_out.get(d->N * d->row));
+        check(hipMemcpy(d_orig, d->h_orig.data(), d->N * d->row, hipMemcpyHostToDevice));
+        check(hipMemcpy(d_rec, d->h_rec.data(), d->M * d->row, hipMemcpyHostToDevice));
+        decode_dev(d->ctx, d->ws, d->high, g, d->N, d->M, d_orig, d->orig_present.data(), d_rec,
+                   d->rec_present.data(), d_out, nullptr);
+        std::vector<uint8_t> padded(d->N * d->row);
+        check(hipMemcpy(padded.data(), d_out, padded.size(), hipMemcpyDeviceToHost));
+        d->h_out.assign(d->N * d->S, 0);
+        for (uint64_t i = 0; i < d->N; ++i)
+            if (!d->orig_present[i]) extract_row(&d->h_out[i * d->S], &padded[i * d->row], d->S);
+        d->has_result = d->decoded = true;
+        return set_err(err, RS_OK);
+    });
+}
+
+const uint8_t *rs_decoder_restored_original(rs_decoder *d, uint64_t index) {
+    if (!d || !d->has_result || !d->decoded || index >= d->N || d->orig_present[index]) return nullptr;
+    return &d->h_out[index * d->S];
+}
+
+uint64_t rs_decoder_restored_count(const rs_decoder *d) {
+    if (!d || !d->has_result || !d->decoded) return 0;
+    return d->N - d->orig_received;
+}
+
+void rs_decoder_result_drop(rs_decoder *d) {
+    if (d) decoder_drop_result(d);
+}
+int rs_decoder_is_high_rate(const rs_decoder *d) { return d ? d->high : -1; }
+void rs_decoder_free(rs_decoder *d) { delete d; }
+
+// ---- one-shot (lib.rs:251-353) -------------------------------------------------
+
+rs_status rs_encode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const uint8_t *const *original,
+                    uint64_t given, uint8_t *recovery_out, rs_error *err) {
+    if (!ctx) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    if (use_high_rate(N, M) < 0) {  // lib.rs:264-269
+        set_err(err, RS_ERR_UNSUPPORTED_SHARD_COUNT);
+        if (err) err->original_count = N, err->recovery_count = M;
+        return RS_ERR_UNSUPPORTED_SHARD_COUNT;
+    }
+    if (given == 0) {  // lib.rs:273-280
+        set_err(err, RS_ERR_TOO_FEW_ORIGINAL_SHARDS);
+        if (err) err->original_count = N, err->original_received_count = 0;
+        return RS_ERR_TOO_FEW_ORIGINAL_SHARDS;
+    }
+    (void)S;  // shard size is inferred from the first shard, as the reference does; S = its length
+    rs_encoder *e = nullptr;
+    rs_status st = rs_encoder_new(ctx, RS_RATE_DEFAULT, N, M, S, &e, err);
+    if (st != RS_OK) return st;
+    for (uint64_t i = 0; i < given && st == RS_OK; ++i) st = rs_encoder_add_original_shard(e, original[i], S, err);
+    if (st == RS_OK) st = rs_encoder_encode(e, err);
+    if (st == RS_OK && recovery_out) std::memcpy(recovery_out, e->h_rec.data(), M * S);
+    rs_encoder_free(e);
+    return st;
+}
+
+rs_status rs_decode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const uint64_t *original_index,
+                    const uint8_t *const *original, uint64_t original_given, const uint64_t *recovery_index,
+                    const uint8_t *const *recovery, uint64_t recovery_given, uint8_t *restored_out,
+                    uint8_t *restored_mask, rs_error *err) {
+    if (!ctx) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    if (restored_mask) std::memset(restored_mask, 0, N);
+    if (use_high_rate(N, M) < 0) {  // lib.rs:310-315
+        set_err(err, RS_ERR_UNSUPPORTED_SHARD_COUNT);
+        if (err) err->original_count = N, err->recovery_count = M;
+        return RS_ERR_UNSUPPORTED_SHARD_COUNT;
+    }
+    if (recovery_given == 0) {  // lib.rs:320-334
+        if (original_given == N) return set_err(err, RS_OK);
+        set_err(err, RS_ERR_NOT_ENOUGH_SHARDS);
+        if (err) err->original_count = N, err->original_received_count = original_given;
+        return RS_ERR_NOT_ENOUGH_SHARDS;
+    }
+    rs_decoder *d = nullptr;
+    rs_status st = rs_decoder_new(ctx, RS_RATE_DEFAULT, N, M, S, &d, err);
+    if (st != RS_OK) return st;
+    // shard lengths are S by construction of this C entry point; per-shard
+    // lengths are checked by the Python / C++ front-ends that know them
+    for (uint64_t i = 0; i < original_given && st == RS_OK; ++i)
+        st = rs_decoder_add_original_shard(d, original_index[i], original[i], S, err);
+    for (uint64_t i = 0; i < recovery_given && st == RS_OK; ++i)
+        st = rs_decoder_add_recovery_shard(d, recovery_index[i], recovery[i], S, err);
+    if (st == RS_OK) st = rs_decoder_decode(d, err);
+    if (st == RS_OK && d->decoded)
+        for (uint64_t i = 0; i < N; ++i)
+            if (!d->orig_present[i]) {
+                if (restored_out) std::memcpy(restored_out + i * S, &d->h_out[i * S], S);
+                if (restored_mask) restored_mask[i] = 1;
+            }
+    rs_decoder_free(d);
+    return st;
+}
+
+// ---- Engine trait on device rows ------------------------------------------------
+
+static rs_status engine_xform(rs_context *ctx, void *rows, uint64_t count, uint64_t len64, uint64_t pos,
+                              uint64_t size, uint64_t trunc, uint64_t delta, void *stream, bool fft) {
+    if (!ctx || !rows || size == 0 || (size & (size - 1)) || pos + size > count || trunc > size ||
+        size > 65536 || delta + size > 65536 + 1)
+        return RS_ERR_INVALID_ARGUMENT;
+    return guarded(nullptr, [&]() -> rs_status {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        const Geom g{len64 * 64, uint32_t(len64 * 8)};
+        uint8_t *base = static_cast<uint8_t *>(rows) + pos * g.stride;
+        auto s = static_cast<hipStream_t>(stream);
+        const uint32_t n = uint32_t(size), L = ilog2(n);
+        rs::PassArgs A = base_args(ctx, g, n);
+        A.ifft_delta = A.fft_delta = uint32_t(delta);
+        const Split sp = split(L);
+        const int flag = fft ? rs::kFft : rs::kIfft;
+        if (sp.single) {
+            A.work_in = A.work_out = base;
+            A.work_stride = g.stride;
+            launch(L, flag, A, 1, 0, s);
+            return RS_OK;
+        }
+        // two passes, in place: FFT = high bits then low bits; IFFT = low then high
+        A.work_in = A.work_out = base;
+        A.work_stride = g.stride;
+        if (fft) {
+            launch(sp.kb, flag, A, 1u << sp.a, sp.a, s);
+            launch(sp.a, flag, A, n >> sp.a, 0, s);
+        } else {
+            launch(sp.a, flag, A, n >> sp.a, 0, s);
+            launch(sp.kb, flag, A, 1u << sp.a, sp.a, s);
+        }
+        return RS_OK;
+    });
+}
+
+rs_status rs_engine_fft(rs_context *ctx, void *d_rows, uint64_t shard_count, uint64_t shard_len_64, uint64_t pos,
+                        uint64_t size, uint64_t truncated_size, uint64_t skew_delta, void *stream) {
+    return engine_xform(ctx, d_rows, shard_count, shard_len_64, pos, size, truncated_size, skew_delta, stream, true);
+}
+rs_status rs_engine_ifft(rs_context *ctx, void *d_rows, uint64_t shard_count, uint64_t shard_len_64, uint64_t pos,
+                         uint64_t size, uint64_t truncated_size, uint64_t skew_delta, void *stream) {
+    return engine_xform(ctx, d_rows, shard_count, shard_len_64, pos, size, truncated_size, skew_delta, stream,
+                        false);
+}
+
+rs_status rs_engine_mul(rs_context *ctx, void *d_rows, uint64_t block_count, uint16_t log_m, void *stream) {
+    if (!ctx || (!d_rows && block_count)) return RS_ERR_INVALID_ARGUMENT;
+    return guarded(nullptr, [&]() -> rs_status {
+        check(rs::launch_mul(static_cast<uint8_t *>(d_rows), block_count, ctx->d_lut + size_t(log_m) * rs::kPermWords,
+                             static_cast<hipStream_t>(stream)));
+        return RS_OK;
+    });
+}
+
+rs_status rs_engine_formal_derivative(rs_context *ctx, void *d_rows, uint64_t count, uint64_t len64, void *stream) {
+    // utils.rs:99-104 slices work[i .. i + lowbit(i)], in range only for 2^k rows
+    if (!ctx || (!d_rows && count) || (count & (count - 1))) return RS_ERR_INVALID_ARGUMENT;
+    return guarded(nullptr, [&]() -> rs_status {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        const uint64_t bytes = count * len64 * 64;
+        auto *tmp = static_cast<uint8_t *>(ctx->ws.work.get(bytes));
+        auto s = static_cast<hipStream_t>(stream);
+        check(hipMemcpyAsync(tmp, d_rows, bytes, hipMemcpyDeviceToDevice, s));
+        check(rs::launch_formal_derivative(tmp, static_cast<uint8_t *>(d_rows), uint32_t(count), len64 * 64, s));
+        return RS_OK;
+    });
+}
+
+void rs_engine_eval_poly(uint16_t *erasures, uint64_t truncated_size) { rs::eval_poly_host(erasures, truncated_size); }
+
+const uint16_t *rs_table_exp(void) { return rs::tables().exp.data(); }
+const uint16_t *rs_table_log(void) { return rs::tables().log.data(); }
+const uint16_t *rs_table_skew(void) { return rs::tables().skew.data(); }
+const uint16_t *rs_table_log_walsh(void) { return rs::tables().log_walsh.data(); }
+const uint32_t *rs_table_perm_by_log(void) { return rs::tables().perm_by_log.data(); }
+const uint32_t *rs_table_perm_by_skew(void) { return rs::tables().perm_by_skew.data(); }
+
+}  // extern "C"

@@ -1,0 +1,77 @@
+// Device-side interface of the MI355X Reed-Solomon engine (host <-> kernels).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace rs {
+
+// A contiguous range of transform rows backed by a caller buffer:
+// transform row r in [row_begin, row_end) lives at base + (r - row_begin) * stride.
+struct RowMap {
+    const uint8_t *base = nullptr;
+    uint64_t stride = 0;
+    uint32_t row_begin = 0, row_end = 0;
+};
+
+// One pass of the multi-pass transform (see DESIGN.md "Pass structure").
+//
+// A workgroup owns one row SET x one 64-pack column SLICE.  A row set is
+// 2^K transform rows whose indices differ only in bits [a, a+K):
+//   row(j) = s_lo + (j << a) + (s_hi << (a + K)),  s = set index, j = local row.
+// A pack is 4 GF(2^16) elements of one row: 4 low bytes at block offset 4p and
+// the matching 4 high bytes at 32 + 4p (reference layout, algorithm.md:18-31).
+struct PassArgs {
+    uint32_t a = 0;        // stride exponent of the row set
+    uint32_t nsets = 1;    // row sets per chunk (n >> K)
+    uint32_t n = 1;        // transform size (rows per chunk)
+    uint32_t packs = 0;    // packs per row (shard_bytes / 8)
+    uint32_t slices = 0;   // ceil(packs / 64)
+    uint32_t grid_chunks = 1;  // chunks spread over gridDim.y
+
+    // ---- load: transform row r = row(j) + chunk * n
+    RowMap src[2];
+    uint32_t nsrc = 0;
+    const uint32_t *rowinfo = nullptr;  // decode: bits 0-15 log factor, bit 16 = erased (row is zero)
+    uint32_t load_scale = 0;            // scale loaded rows by rowinfo (erased rows load as zero)
+    const uint8_t *work_in = nullptr;   // if set, rows come from work_in + r * work_stride
+    uint64_t work_stride = 0;
+    uint32_t in_chunks = 1;             // in-kernel XOR accumulation over chunks
+
+    // ---- transforms
+    uint32_t ifft_delta = 0, ifft_delta_step = 0;
+    uint32_t fd_mode = 0;               // 0: none, 1: sum_b P_b over local bits, 2: identity + that
+    const uint8_t *xor_in = nullptr;    // after fd: x ^= rows of xor_in (stride work_stride)
+    uint32_t fft_delta = 0, fft_delta_step = 0;
+    uint32_t out_chunks = 1;            // FFT + store repeated per output chunk
+
+    // ---- store: transform row r = row(j) + chunk * n
+    uint8_t *work_out = nullptr;        // if set, every row goes to work_out + r * work_stride
+    RowMap dst;                         // else rows in [row_begin, row_end) go to dst
+    uint32_t reveal = 0;                // store only erased rows, scaled by exp(65535 - factor)
+
+    const uint32_t *tw = nullptr;       // perm tables indexed by skew index (zero table = no multiply)
+    const uint32_t *lut = nullptr;      // perm tables indexed by log factor
+};
+
+enum PassFlags { kIfft = 1, kFft = 2 };
+
+// Launch one pass on `stream`.  K = log2(rows per set).
+hipError_t launch_pass(int K, int flags, const PassArgs &args, hipStream_t stream);
+
+// eval_poly for a decode: erasure vector -> per-row log factors.
+//   state[r] (r < 2^u): bit0 = erasure-vector entry, bit1 = row received.
+//   low_rate: the erasure vector is also 1 on [2^u, 65536) (rate_low.rs:196).
+//   end: recovery_end / original_end (rows >= end are zero in the vector for high rate).
+hipError_t launch_eval_poly(uint32_t u, bool low_rate, uint32_t end, const uint8_t *state,
+                            const uint16_t *lw_fold_u, uint16_t log_walsh0, uint32_t *rowinfo,
+                            hipStream_t stream);
+
+// x[rows] *= exp(log_m) over `blocks` 64-byte blocks.
+hipError_t launch_mul(uint8_t *rows, uint64_t blocks, const uint32_t *lut_entry, hipStream_t stream);
+
+// out[q] = in[q] ^ XOR_{b: q_b = 0, 2^b < rows} in[q | 2^b]  (formal derivative, closed form)
+hipError_t launch_formal_derivative(const uint8_t *in, uint8_t *out, uint32_t rows, uint64_t row_bytes,
+                                    hipStream_t stream);
+
+}  // namespace rs

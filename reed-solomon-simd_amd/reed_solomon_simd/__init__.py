@@ -1,0 +1,632 @@
+"""reed_solomon_simd -- MI355X-native drop-in for the reed-solomon-simd API.
+
+Python mirror of the reference crate's public interface (AndersTrier/
+reed-solomon-simd v3.1.0, /root/reference):
+
+    encode(original_count, recovery_count, original)            src/lib.rs:251-290
+    decode(original_count, recovery_count, original, recovery)  src/lib.rs:292-353
+    ReedSolomonEncoder / ReedSolomonDecoder                      src/reed_solomon.rs
+    EncoderResult / DecoderResult                                src/encoder_result.rs, decoder_result.rs
+    Error (one subclass per variant, same fields)               src/lib.rs:48-231
+    rate.{DefaultRate, HighRate, LowRate}{Encoder,Decoder}       src/rate/*.rs
+
+plus the device-resident batch path `encode_device` / `decode_device` that
+works on HIP device pointers (e.g. torch tensors on cuda:0).
+
+Everything runs through the C ABI of librs_mi355x.so (include/rs_mi355x.h);
+there is no CPU fallback: importing fails loudly if the library is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, Iterable, List, Optional, Tuple
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librs_mi355x.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} not built; run `python -c 'import __graft_entry__ as g; g.build()'` (HIP extension required)"
+    )
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+_u64 = ctypes.c_uint64
+_vp = ctypes.c_void_p
+_int = ctypes.c_int
+
+
+class _RsError(ctypes.Structure):
+    _fields_ = [
+        ("code", ctypes.c_int32),
+        ("original_count", _u64),
+        ("recovery_count", _u64),
+        ("shard_bytes", _u64),
+        ("got", _u64),
+        ("index", _u64),
+        ("original_received_count", _u64),
+        ("recovery_received_count", _u64),
+    ]
+
+
+_E = ctypes.POINTER(_RsError)
+
+
+def _sig(name, restype, *args):
+    f = getattr(_lib, name)
+    f.restype = restype
+    f.argtypes = list(args)
+    return f
+
+
+_sig("rs_context_create", _int, _int, ctypes.POINTER(_vp))
+_sig("rs_context_destroy", None, _vp)
+_sig("rs_last_device_error", ctypes.c_char_p)
+_sig("rs_version", ctypes.c_char_p)
+_sig("rs_supports", _int, _int, _u64, _u64)
+_sig("rs_use_high_rate", _int, _u64, _u64)
+_sig("rs_validate", _int, _int, _u64, _u64, _u64, _E)
+_sig("rs_encoder_work_count", _u64, _int, _u64, _u64)
+_sig("rs_decoder_work_count", _u64, _int, _u64, _u64)
+_sig("rs_encoder_new", _int, _vp, _int, _u64, _u64, _u64, ctypes.POINTER(_vp), _E)
+_sig("rs_encoder_reset", _int, _vp, _u64, _u64, _u64, _E)
+_sig("rs_encoder_add_original_shard", _int, _vp, ctypes.c_char_p, _u64, _E)
+_sig("rs_encoder_encode", _int, _vp, _E)
+_sig("rs_encoder_recovery", ctypes.POINTER(ctypes.c_uint8), _vp, _u64)
+_sig("rs_encoder_result_drop", None, _vp)
+_sig("rs_encoder_is_high_rate", _int, _vp)
+_sig("rs_encoder_free", None, _vp)
+_sig("rs_decoder_new", _int, _vp, _int, _u64, _u64, _u64, ctypes.POINTER(_vp), _E)
+_sig("rs_decoder_reset", _int, _vp, _u64, _u64, _u64, _E)
+_sig("rs_decoder_add_original_shard", _int, _vp, _u64, ctypes.c_char_p, _u64, _E)
+_sig("rs_decoder_add_recovery_shard", _int, _vp, _u64, ctypes.c_char_p, _u64, _E)
+_sig("rs_decoder_decode", _int, _vp, _E)
+_sig("rs_decoder_restored_original", ctypes.POINTER(ctypes.c_uint8), _vp, _u64)
+_sig("rs_decoder_restored_count", _u64, _vp)
+_sig("rs_decoder_result_drop", None, _vp)
+_sig("rs_decoder_is_high_rate", _int, _vp)
+_sig("rs_decoder_free", None, _vp)
+_sig("rs_encode_device", _int, _vp, _int, _u64, _u64, _u64, _vp, _vp, _vp, _E)
+_sig("rs_decode_device", _int, _vp, _int, _u64, _u64, _u64, _vp, ctypes.c_char_p, _vp, ctypes.c_char_p, _vp, _vp, _E)
+_sig("rs_engine_fft", _int, _vp, _vp, _u64, _u64, _u64, _u64, _u64, _u64, _vp)
+_sig("rs_engine_ifft", _int, _vp, _vp, _u64, _u64, _u64, _u64, _u64, _u64, _vp)
+_sig("rs_engine_mul", _int, _vp, _vp, _u64, ctypes.c_uint16, _vp)
+_sig("rs_engine_eval_poly", None, ctypes.POINTER(ctypes.c_uint16), _u64)
+_sig("rs_engine_formal_derivative", _int, _vp, _vp, _u64, _u64, _vp)
+for _t in ("exp", "log", "skew", "log_walsh"):
+    _sig(f"rs_table_{_t}", ctypes.POINTER(ctypes.c_uint16))
+for _t in ("perm_by_log", "perm_by_skew"):
+    _sig(f"rs_table_{_t}", ctypes.POINTER(ctypes.c_uint32))
+
+GF_BITS = 16
+GF_ORDER = 65536
+GF_MODULUS = 65535
+
+RATE_DEFAULT, RATE_HIGH, RATE_LOW = 0, 1, 2
+
+
+# ---------------------------------------------------------------------------
+# Errors (src/lib.rs:48-142)
+
+class Error(Exception):
+    """Base of the reference's `Error` variants; fields as attributes."""
+
+    fields: Tuple[str, ...] = ()
+
+    def __init__(self, **kw):
+        for f in self.fields:
+            setattr(self, f, kw.get(f))
+        super().__init__(self._msg())
+
+    def _msg(self):
+        return type(self).__name__
+
+    def __eq__(self, other):
+        return type(self) is type(other) and all(getattr(self, f) == getattr(other, f) for f in self.fields)
+
+    def __hash__(self):
+        return hash((type(self).__name__,) + tuple(getattr(self, f) for f in self.fields))
+
+    def __repr__(self):
+        return f"{type(self).__name__}({', '.join(f'{f}={getattr(self, f)}' for f in self.fields)})"
+
+
+class DifferentShardSize(Error):
+    fields = ("shard_bytes", "got")
+
+    def _msg(self):
+        return f"different shard size: expected {self.shard_bytes} bytes, got {self.got} bytes"
+
+
+class DuplicateOriginalShardIndex(Error):
+    fields = ("index",)
+
+    def _msg(self):
+        return f"duplicate original shard index: {self.index}"
+
+
+class DuplicateRecoveryShardIndex(Error):
+    fields = ("index",)
+
+    def _msg(self):
+        return f"duplicate recovery shard index: {self.index}"
+
+
+class InvalidOriginalShardIndex(Error):
+    fields = ("original_count", "index")
+
+    def _msg(self):
+        return f"invalid original shard index: {self.index} >= original_count {self.original_count}"
+
+
+class InvalidRecoveryShardIndex(Error):
+    fields = ("recovery_count", "index")
+
+    def _msg(self):
+        return f"invalid recovery shard index: {self.index} >= recovery_count {self.recovery_count}"
+
+
+class InvalidShardSize(Error):
+    fields = ("shard_bytes",)
+
+    def _msg(self):
+        return f"invalid shard size: {self.shard_bytes} bytes (must non-zero and multiple of 2)"
+
+
+class NotEnoughShards(Error):
+    fields = ("original_count", "original_received_count", "recovery_received_count")
+
+    def _msg(self):
+        return (f"not enough shards: {self.original_received_count} original + {self.recovery_received_count} "
+                f"recovery < {self.original_count} original_count")
+
+
+class TooFewOriginalShards(Error):
+    fields = ("original_count", "original_received_count")
+
+    def _msg(self):
+        return (f"too few original shards: got {self.original_received_count} shards while original_count is "
+                f"{self.original_count}")
+
+
+class TooManyOriginalShards(Error):
+    fields = ("original_count",)
+
+    def _msg(self):
+        return f"too many original shards: got more than original_count ({self.original_count}) shards"
+
+
+class UnsupportedShardCount(Error):
+    fields = ("original_count", "recovery_count")
+
+    def _msg(self):
+        return (f"unsupported shard count: {self.original_count} original shards with {self.recovery_count} "
+                f"recovery shards")
+
+
+class DeviceError(RuntimeError):
+    pass
+
+
+_BY_CODE = {1: DifferentShardSize, 2: DuplicateOriginalShardIndex, 3: DuplicateRecoveryShardIndex,
+            4: InvalidOriginalShardIndex, 5: InvalidRecoveryShardIndex, 6: InvalidShardSize, 7: NotEnoughShards,
+            8: TooFewOriginalShards, 9: TooManyOriginalShards, 10: UnsupportedShardCount}
+
+
+def _raise(code: int, err: _RsError):
+    if code == 0:
+        return
+    cls = _BY_CODE.get(code)
+    if cls is not None:
+        raise cls(**{f: int(getattr(err, f)) for f in cls.fields})
+    if code == 100:
+        raise DeviceError(_lib.rs_last_device_error().decode())
+    raise ValueError(f"invalid argument (rs_status {code})")
+
+
+# ---------------------------------------------------------------------------
+# Context: one per device (GF tables live in HBM)
+
+class Context:
+    def __init__(self, device: int = 0):
+        h = _vp()
+        code = _lib.rs_context_create(device, ctypes.byref(h))
+        if code:
+            raise DeviceError(_lib.rs_last_device_error().decode())
+        self._h = h
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            _lib.rs_context_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_default_ctx: Dict[int, Context] = {}
+
+
+def default_context(device: int = 0) -> Context:
+    if device not in _default_ctx:
+        _default_ctx[device] = Context(device)
+    return _default_ctx[device]
+
+
+def version() -> str:
+    return _lib.rs_version().decode()
+
+
+# ---------------------------------------------------------------------------
+# Encoder / decoder objects (src/reed_solomon.rs, src/rate.rs)
+
+class EncoderResult:
+    """Borrowed view of the recovery shards (src/encoder_result.rs)."""
+
+    def __init__(self, enc: "_EncoderBase"):
+        self._enc = enc
+        self._alive = True
+
+    def recovery(self, index: int) -> Optional[bytes]:
+        if not self._alive:
+            raise RuntimeError("EncoderResult used after drop")
+        p = _lib.rs_encoder_recovery(self._enc._h, index)
+        if not p:
+            return None
+        return ctypes.string_at(p, self._enc.shard_bytes)
+
+    def recovery_iter(self):
+        i = 0
+        while True:
+            r = self.recovery(i)
+            if r is None:
+                return
+            yield r
+            i += 1
+
+    def drop(self):
+        """EncoderResult::drop -> reset_received (encoder_result.rs:48-52)."""
+        if self._alive:
+            self._alive = False
+            _lib.rs_encoder_result_drop(self._enc._h)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.drop()
+
+    def __del__(self):
+        try:
+            self.drop()
+        except Exception:
+            pass
+
+
+class DecoderResult:
+    """Borrowed view of the restored originals (src/decoder_result.rs)."""
+
+    def __init__(self, dec: "_DecoderBase"):
+        self._dec = dec
+        self._alive = True
+
+    def restored_original(self, index: int) -> Optional[bytes]:
+        if not self._alive:
+            raise RuntimeError("DecoderResult used after drop")
+        p = _lib.rs_decoder_restored_original(self._dec._h, index)
+        if not p:
+            return None
+        return ctypes.string_at(p, self._dec.shard_bytes)
+
+    def restored_original_iter(self):
+        for i in range(self._dec.original_count):
+            r = self.restored_original(i)
+            if r is not None:
+                yield i, r
+
+    def __len__(self):
+        return int(_lib.rs_decoder_restored_count(self._dec._h))
+
+    def drop(self):
+        if self._alive:
+            self._alive = False
+            _lib.rs_decoder_result_drop(self._dec._h)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.drop()
+
+    def __del__(self):
+        try:
+            self.drop()
+        except Exception:
+            pass
+
+
+class _EncoderBase:
+    RATE = RATE_DEFAULT
+
+    def __init__(self, original_count: int, recovery_count: int, shard_bytes: int, ctx: Optional[Context] = None):
+        self._ctx = ctx or default_context()
+        h = _vp()
+        err = _RsError()
+        code = _lib.rs_encoder_new(self._ctx.handle, self.RATE, original_count, recovery_count, shard_bytes,
+                                   ctypes.byref(h), ctypes.byref(err))
+        _raise(code, err)
+        self._h = h
+        self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
+        self._result: Optional[EncoderResult] = None
+
+    @classmethod
+    def supports(cls, original_count: int, recovery_count: int) -> bool:
+        return bool(_lib.rs_supports(cls.RATE, original_count, recovery_count))
+
+    @classmethod
+    def validate(cls, original_count: int, recovery_count: int, shard_bytes: int) -> None:
+        err = _RsError()
+        _raise(_lib.rs_validate(cls.RATE, original_count, recovery_count, shard_bytes, ctypes.byref(err)), err)
+
+    @classmethod
+    def work_count(cls, original_count: int, recovery_count: int) -> int:
+        return int(_lib.rs_encoder_work_count(cls.RATE, original_count, recovery_count))
+
+    def _drop_result(self):
+        if self._result is not None:
+            self._result.drop()
+            self._result = None
+
+    def add_original_shard(self, shard) -> None:
+        self._drop_result()
+        b = bytes(shard)
+        err = _RsError()
+        _raise(_lib.rs_encoder_add_original_shard(self._h, b, len(b), ctypes.byref(err)), err)
+
+    def encode(self) -> EncoderResult:
+        err = _RsError()
+        _raise(_lib.rs_encoder_encode(self._h, ctypes.byref(err)), err)
+        self._result = EncoderResult(self)
+        return self._result
+
+    def reset(self, original_count: int, recovery_count: int, shard_bytes: int) -> None:
+        self._drop_result()
+        err = _RsError()
+        _raise(_lib.rs_encoder_reset(self._h, original_count, recovery_count, shard_bytes, ctypes.byref(err)), err)
+        self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
+
+    @property
+    def is_high_rate(self) -> bool:
+        return bool(_lib.rs_encoder_is_high_rate(self._h))
+
+    def __del__(self):
+        try:
+            if self._h:
+                _lib.rs_encoder_free(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+class _DecoderBase:
+    RATE = RATE_DEFAULT
+
+    def __init__(self, original_count: int, recovery_count: int, shard_bytes: int, ctx: Optional[Context] = None):
+        self._ctx = ctx or default_context()
+        h = _vp()
+        err = _RsError()
+        code = _lib.rs_decoder_new(self._ctx.handle, self.RATE, original_count, recovery_count, shard_bytes,
+                                   ctypes.byref(h), ctypes.byref(err))
+        _raise(code, err)
+        self._h = h
+        self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
+        self._result: Optional[DecoderResult] = None
+
+    supports = classmethod(lambda cls, n, m: bool(_lib.rs_supports(cls.RATE, n, m)))
+
+    @classmethod
+    def validate(cls, original_count: int, recovery_count: int, shard_bytes: int) -> None:
+        err = _RsError()
+        _raise(_lib.rs_validate(cls.RATE, original_count, recovery_count, shard_bytes, ctypes.byref(err)), err)
+
+    @classmethod
+    def work_count(cls, original_count: int, recovery_count: int) -> int:
+        return int(_lib.rs_decoder_work_count(cls.RATE, original_count, recovery_count))
+
+    def _drop_result(self):
+        if self._result is not None:
+            self._result.drop()
+            self._result = None
+
+    def add_original_shard(self, index: int, shard) -> None:
+        self._drop_result()
+        b = bytes(shard)
+        err = _RsError()
+        _raise(_lib.rs_decoder_add_original_shard(self._h, index, b, len(b), ctypes.byref(err)), err)
+
+    def add_recovery_shard(self, index: int, shard) -> None:
+        self._drop_result()
+        b = bytes(shard)
+        err = _RsError()
+        _raise(_lib.rs_decoder_add_recovery_shard(self._h, index, b, len(b), ctypes.byref(err)), err)
+
+    def decode(self) -> DecoderResult:
+        err = _RsError()
+        _raise(_lib.rs_decoder_decode(self._h, ctypes.byref(err)), err)
+        self._result = DecoderResult(self)
+        return self._result
+
+    def reset(self, original_count: int, recovery_count: int, shard_bytes: int) -> None:
+        self._drop_result()
+        err = _RsError()
+        _raise(_lib.rs_decoder_reset(self._h, original_count, recovery_count, shard_bytes, ctypes.byref(err)), err)
+        self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
+
+    @property
+    def is_high_rate(self) -> bool:
+        return bool(_lib.rs_decoder_is_high_rate(self._h))
+
+    def __del__(self):
+        try:
+            if self._h:
+                _lib.rs_decoder_free(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+class ReedSolomonEncoder(_EncoderBase):
+    """src/reed_solomon.rs:13-81 (DefaultRate + the MI355X engine)."""
+
+
+class ReedSolomonDecoder(_DecoderBase):
+    """src/reed_solomon.rs:83-183."""
+
+
+class _RateNS:
+    pass
+
+
+rate = _RateNS()
+for _name, _r in (("Default", RATE_DEFAULT), ("High", RATE_HIGH), ("Low", RATE_LOW)):
+    setattr(rate, f"{_name}RateEncoder", type(f"{_name}RateEncoder", (_EncoderBase,), {"RATE": _r}))
+    setattr(rate, f"{_name}RateDecoder", type(f"{_name}RateDecoder", (_DecoderBase,), {"RATE": _r}))
+
+
+# ---------------------------------------------------------------------------
+# one-shot (src/lib.rs:251-353)
+
+def encode(original_count: int, recovery_count: int, original: Iterable) -> List[bytes]:
+    if not ReedSolomonEncoder.supports(original_count, recovery_count):
+        raise UnsupportedShardCount(original_count=original_count, recovery_count=recovery_count)
+    it = iter(original)
+    try:
+        first = bytes(next(it))
+    except StopIteration:
+        raise TooFewOriginalShards(original_count=original_count, original_received_count=0) from None
+    enc = ReedSolomonEncoder(original_count, recovery_count, len(first))
+    enc.add_original_shard(first)
+    for s in it:
+        enc.add_original_shard(s)
+    res = enc.encode()
+    out = list(res.recovery_iter())
+    res.drop()
+    return out
+
+
+def decode(original_count: int, recovery_count: int, original: Iterable[Tuple[int, bytes]],
+           recovery: Iterable[Tuple[int, bytes]]) -> Dict[int, bytes]:
+    if not ReedSolomonDecoder.supports(original_count, recovery_count):
+        raise UnsupportedShardCount(original_count=original_count, recovery_count=recovery_count)
+    original = list(original)
+    rit = iter(recovery)
+    try:
+        first = next(rit)
+    except StopIteration:
+        if len(original) == original_count:
+            return {}
+        raise NotEnoughShards(original_count=original_count, original_received_count=len(original),
+                              recovery_received_count=0) from None
+    shard_bytes = len(bytes(first[1]))
+    dec = ReedSolomonDecoder(original_count, recovery_count, shard_bytes)
+    for i, s in original:
+        dec.add_original_shard(i, s)
+    dec.add_recovery_shard(first[0], first[1])
+    for i, s in rit:
+        dec.add_recovery_shard(i, s)
+    res = dec.decode()
+    out = dict(res.restored_original_iter())
+    res.drop()
+    return out
+
+
+# ---------------------------------------------------------------------------
+# device-resident path (HIP device pointers; torch tensors accepted)
+
+def _ptr(x) -> int:
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    return int(x)
+
+
+def _stream(stream) -> Optional[int]:
+    if stream is None:
+        return None
+    if hasattr(stream, "cuda_stream"):
+        return stream.cuda_stream
+    return int(stream)
+
+
+def encode_device(original_count: int, recovery_count: int, shard_bytes: int, d_original, d_recovery,
+                  stream=None, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None) -> None:
+    ctx = ctx or default_context()
+    err = _RsError()
+    _raise(_lib.rs_encode_device(ctx.handle, rate_, original_count, recovery_count, shard_bytes, _ptr(d_original),
+                                 _ptr(d_recovery), _stream(stream), ctypes.byref(err)), err)
+
+
+def decode_device(original_count: int, recovery_count: int, shard_bytes: int, d_original, original_present,
+                  d_recovery, recovery_present, d_restored, stream=None, rate_: int = RATE_DEFAULT,
+                  ctx: Optional[Context] = None) -> None:
+    ctx = ctx or default_context()
+    op = bytes(bytearray(1 if x else 0 for x in original_present))
+    rp = bytes(bytearray(1 if x else 0 for x in recovery_present))
+    err = _RsError()
+    _raise(_lib.rs_decode_device(ctx.handle, rate_, original_count, recovery_count, shard_bytes, _ptr(d_original), op,
+                                 _ptr(d_recovery), rp, _ptr(d_restored), _stream(stream), ctypes.byref(err)), err)
+
+
+class engine:
+    """trait Engine over device shard matrices (src/engine.rs:234-291)."""
+
+    @staticmethod
+    def fft(d_rows, shard_count, shard_len_64, pos, size, truncated_size, skew_delta, stream=None, ctx=None):
+        ctx = ctx or default_context()
+        code = _lib.rs_engine_fft(ctx.handle, _ptr(d_rows), shard_count, shard_len_64, pos, size, truncated_size,
+                                  skew_delta, _stream(stream))
+        _raise(code, _RsError())
+
+    @staticmethod
+    def ifft(d_rows, shard_count, shard_len_64, pos, size, truncated_size, skew_delta, stream=None, ctx=None):
+        ctx = ctx or default_context()
+        code = _lib.rs_engine_ifft(ctx.handle, _ptr(d_rows), shard_count, shard_len_64, pos, size, truncated_size,
+                                   skew_delta, _stream(stream))
+        _raise(code, _RsError())
+
+    @staticmethod
+    def mul(d_rows, block_count, log_m, stream=None, ctx=None):
+        ctx = ctx or default_context()
+        _raise(_lib.rs_engine_mul(ctx.handle, _ptr(d_rows), block_count, log_m, _stream(stream)), _RsError())
+
+    @staticmethod
+    def formal_derivative(d_rows, shard_count, shard_len_64, stream=None, ctx=None):
+        ctx = ctx or default_context()
+        _raise(_lib.rs_engine_formal_derivative(ctx.handle, _ptr(d_rows), shard_count, shard_len_64,
+                                                _stream(stream)), _RsError())
+
+    @staticmethod
+    def eval_poly(erasures, truncated_size):
+        """In place on a writable buffer of 65536 uint16 (e.g. numpy array)."""
+        import numpy as np
+        a = np.ascontiguousarray(erasures, dtype=np.uint16)
+        _lib.rs_engine_eval_poly(a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), truncated_size)
+        return a
+
+
+def table(name: str, count: int):
+    import numpy as np
+    p = getattr(_lib, f"rs_table_{name}")()
+    return np.ctypeslib.as_array(p, shape=(count,)).copy()
+
+
+def use_high_rate(original_count: int, recovery_count: int) -> int:
+    return int(_lib.rs_use_high_rate(original_count, recovery_count))

@@ -1,0 +1,448 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bit-exact comparisons at oracle-sized configurations, the reference's golden
+SHA-256 vectors through the drop-in API, the reference's error semantics, and
+size-independent properties at BASELINE.json's full sizes (encode -> erase ->
+decode round trips, and column-sampled comparisons: every engine op is
+column-wise, so encoding 64-byte column blocks of a large shard matrix on the
+CPU must reproduce the same columns of the GPU result).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden_cases.json")))
+RATE = {"default": 0, "high": 1, "low": 2}
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.skip("no GPU")
+    return t
+
+
+@pytest.fixture(scope="module")
+def rs(torch):
+    import reed_solomon_simd
+    return reed_solomon_simd
+
+
+def _dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def gpu_encode(torch, rs, rate, orig, M):
+    N, S = orig.shape
+    d_orig = _dev(torch, orig)
+    d_rec = torch.full((M, S), 0xEE, dtype=torch.uint8, device="cuda")
+    rs.encode_device(N, M, S, d_orig, d_rec, rate_=RATE[rate])
+    torch.cuda.synchronize()
+    return d_rec.cpu().numpy()
+
+
+def gpu_decode(torch, rs, rate, orig, op, rec, rp):
+    N, S = orig.shape
+    M = rec.shape[0]
+    d_o = _dev(torch, np.where(op[:, None] == 1, orig, 0xA5).astype(np.uint8))
+    d_r = _dev(torch, np.where(rp[:, None] == 1, rec, 0x5A).astype(np.uint8))
+    d_out = torch.full((N, S), 0x33, dtype=torch.uint8, device="cuda")
+    rs.decode_device(N, M, S, d_o, op, d_r, rp, d_out, rate_=RATE[rate])
+    torch.cuda.synchronize()
+    return d_out.cpu().numpy()
+
+
+# ---------------------------------------------------------------------------
+# device-resident path vs oracle, bit-exact
+
+ENC_CASES = [
+    # (rate, N, M, S) -- single-pass (n <= 256), multi-pass (n > 256), multi-chunk
+    ("default", 1, 1, 64), ("default", 3, 5, 64), ("high", 5, 3, 128), ("low", 3, 5, 128),
+    ("default", 64, 64, 1024), ("default", 100, 37, 192), ("default", 37, 100, 320),
+    ("high", 1000, 100, 128), ("low", 100, 1000, 128), ("default", 1024, 1024, 1024),
+    ("default", 1000, 1000, 576), ("high", 3000, 700, 64), ("low", 700, 3000, 64),
+    ("default", 5000, 300, 256), ("default", 300, 5000, 256), ("default", 4096, 4096, 512),
+    ("default", 10000, 1000, 128), ("high", 32768, 32768, 64), ("low", 32768, 32768, 64),
+    ("high", 61440, 4096, 64), ("low", 4096, 61440, 64),
+]
+
+
+@pytest.mark.parametrize("rate,N,M,S", ENC_CASES)
+def test_encode_device_matches_oracle(torch, rs, rate, N, M, S):
+    orig = O.generate_original(N, S, (N * 31 + M) & 0xFF)
+    want = O.encode(rate, orig, M)
+    got = gpu_encode(torch, rs, rate, orig, M)
+    assert np.array_equal(got, want)
+
+
+DEC_CASES = [
+    ("default", 3, 5, 64, 0.5), ("high", 5, 3, 128, 0.5), ("low", 3, 5, 128, 1.0), ("default", 64, 64, 1024, 0.3),
+    ("default", 100, 37, 192, 0.2), ("default", 37, 100, 320, 1.0), ("default", 1024, 1024, 1024, 0.01),
+    ("default", 1024, 1024, 1024, 1.0), ("high", 1000, 100, 128, 0.1), ("low", 100, 1000, 128, 0.9),
+    ("default", 3000, 700, 64, 0.2), ("low", 700, 3000, 64, 0.5), ("default", 4096, 4096, 512, 0.5),
+    ("high", 32768, 32768, 64, 1.0), ("low", 32768, 32768, 64, 0.3), ("high", 61440, 4096, 64, 0.05),
+]
+
+
+@pytest.mark.parametrize("rate,N,M,S,loss", DEC_CASES)
+def test_decode_device_matches_oracle(torch, rs, rate, N, M, S, loss):
+    rng = np.random.default_rng(N + 3 * M)
+    orig = O.generate_original(N, S, 5)
+    rec = O.encode(rate, orig, M)
+    L = max(1, int(round(min(N, M) * loss)))
+    op = np.ones(N, np.uint8)
+    op[rng.choice(N, L, replace=False)] = 0
+    rp = np.zeros(M, np.uint8)
+    rp[rng.choice(M, L, replace=False)] = 1
+    want = O.decode(rate, orig, op, rec, rp)
+    got = gpu_decode(torch, rs, rate, orig, op, rec, rp)
+    miss = op == 0
+    assert np.array_equal(got[miss], orig[miss])
+    assert np.array_equal(got[miss], want[miss])
+    assert np.all(got[~miss] == 0x33), "present rows of the output must not be written"
+
+
+# ---------------------------------------------------------------------------
+# the reference's golden vectors through the drop-in object API
+
+def _run_golden(rs, c):
+    n, m, s = c["original_count"], c["recovery_count"], c["shard_bytes"]
+    orig = O.generate_original(n, s, c["seed"])
+    cls = {"default": rs.rate.DefaultRateEncoder, "high": rs.rate.HighRateEncoder,
+           "low": rs.rate.LowRateEncoder}[c["rate"]]
+    dcls = {"default": rs.rate.DefaultRateDecoder, "high": rs.rate.HighRateDecoder,
+            "low": rs.rate.LowRateDecoder}[c["rate"]]
+    enc = cls(n, m, s)
+    for row in orig:
+        enc.add_original_shard(row.tobytes())
+    res = enc.encode()
+    rec = list(res.recovery_iter())
+    assert hashlib.sha256(b"".join(rec)).hexdigest() == c["recovery_sha256"], c["source"]
+    dec = dcls(n, m, s)
+    got = np.zeros(n, bool)
+    for a, b in c["decoder_original"]:
+        for i in range(a, b):
+            dec.add_original_shard(i, orig[i].tobytes())
+            got[i] = True
+    for a, b in c["decoder_recovery"]:
+        for i in range(a, b):
+            dec.add_recovery_shard(i, rec[i])
+    r = dec.decode()
+    restored = dict(r.restored_original_iter())
+    for i in np.where(~got)[0]:
+        assert restored[int(i)] == orig[i].tobytes(), (c["source"], int(i))
+
+
+@pytest.mark.parametrize("case", [pytest.param(c, id=c["name"]) for c in GOLD["single"]])
+def test_golden_vectors_object_api(rs, case):
+    _run_golden(rs, case)
+
+
+@pytest.mark.parametrize("seq", [pytest.param(s, id=s["name"]) for s in GOLD["two_rounds"]])
+def test_two_rounds(rs, seq):
+    """roundtrip_two_rounds! (test_util.rs:211-364): work re-use with implicit or explicit reset."""
+    enc_cls = {"default": rs.rate.DefaultRateEncoder, "high": rs.rate.HighRateEncoder,
+               "low": rs.rate.LowRateEncoder}[seq["rate"]]
+    dec_cls = {"default": rs.rate.DefaultRateDecoder, "high": rs.rate.HighRateDecoder,
+               "low": rs.rate.LowRateDecoder}[seq["rate"]]
+    r0 = seq["rounds"][0]
+    enc = enc_cls(r0["original_count"], r0["recovery_count"], r0["shard_bytes"])
+    dec = dec_cls(r0["original_count"], r0["recovery_count"], r0["shard_bytes"])
+    for k, r in enumerate(seq["rounds"]):
+        if k and seq["explicit_reset"]:
+            enc.reset(r["original_count"], r["recovery_count"], r["shard_bytes"])
+            dec.reset(r["original_count"], r["recovery_count"], r["shard_bytes"])
+        orig = O.generate_original(r["original_count"], r["shard_bytes"], r["seed"])
+        for row in orig:
+            enc.add_original_shard(row.tobytes())
+        res = enc.encode()
+        rec = list(res.recovery_iter())
+        res.drop()
+        assert hashlib.sha256(b"".join(rec)).hexdigest() == r["recovery_sha256"]
+        have = set()
+        for a, b in r["decoder_original"]:
+            for i in range(a, b):
+                dec.add_original_shard(i, orig[i].tobytes())
+                have.add(i)
+        for a, b in r["decoder_recovery"]:
+            for i in range(a, b):
+                dec.add_recovery_shard(i, rec[i])
+        out = dec.decode()
+        for i in range(r["original_count"]):
+            if i not in have:
+                assert out.restored_original(i) == orig[i].tobytes()
+        out.drop()
+
+
+def test_readme_example(rs):
+    """README.md:87-115: 3 original x 64 B, 5 recovery; restore #0 and #2."""
+    original = [b"Lorem ipsum dolor sit amet, consectetur adipiscing elit, sed do ",
+                b"eiusmod tempor incididunt ut labore et dolore magna aliqua. Ut e",
+                b"nim ad minim veniam, quis nostrud exercitation ullamco laboris n"]
+    recovery = rs.encode(3, 5, original)
+    want = O.encode("default", np.frombuffer(b"".join(original), np.uint8).reshape(3, 64), 5)
+    assert b"".join(recovery) == want.tobytes()
+    restored = rs.decode(3, 5, [(1, original[1])], [(1, recovery[1]), (4, recovery[4])])
+    assert restored == {0: original[0], 2: original[2]}
+
+
+@pytest.mark.parametrize("S", [2, 4, 6, 30, 32, 34, 62, 64, 66, 126, 128, 130])
+def test_shard_size_not_divisible_by_64(rs, S):
+    """decoder_result.rs:166-171 sizes; tail re-pack (shards.rs:38-74) vs the oracle."""
+    orig = O.generate_original(3, S, 0)
+    want = O.encode("default", orig, 2)
+    enc = rs.ReedSolomonEncoder(3, 2, S)
+    for row in orig:
+        enc.add_original_shard(row.tobytes())
+    res = enc.encode()
+    rec = list(res.recovery_iter())
+    assert b"".join(rec) == want.tobytes()
+    dec = rs.ReedSolomonDecoder(3, 2, S)
+    dec.add_original_shard(1, orig[1].tobytes())
+    dec.add_recovery_shard(0, rec[0])
+    dec.add_recovery_shard(1, rec[1])
+    out = dec.decode()
+    assert out.restored_original(0) == orig[0].tobytes()
+    assert out.restored_original(1) is None
+    assert out.restored_original(2) == orig[2].tobytes()
+    assert out.restored_original(3) is None
+    assert list(out.restored_original_iter()) == [(0, orig[0].tobytes()), (2, orig[2].tobytes())]
+
+
+# ---------------------------------------------------------------------------
+# error semantics (test_util.rs:369-573, lib.rs:420-617)
+
+@pytest.mark.parametrize("which", ["default", "high", "low"])
+def test_encoder_errors(rs, which):
+    E = {"default": rs.rate.DefaultRateEncoder, "high": rs.rate.HighRateEncoder, "low": rs.rate.LowRateEncoder}[which]
+    enc = E(1, 1, 64)
+    with pytest.raises(rs.DifferentShardSize) as e:
+        enc.add_original_shard(bytes(128))
+    assert e.value == rs.DifferentShardSize(shard_bytes=64, got=128)
+    with pytest.raises(rs.InvalidShardSize) as e:
+        E(1, 1, 123)
+    assert e.value == rs.InvalidShardSize(shard_bytes=123)
+    with pytest.raises(rs.InvalidShardSize):
+        E(1, 1, 64).reset(1, 1, 123)
+    with pytest.raises(rs.TooFewOriginalShards) as e:
+        E(1, 1, 64).encode()
+    assert e.value == rs.TooFewOriginalShards(original_count=1, original_received_count=0)
+    enc = E(1, 1, 64)
+    enc.add_original_shard(bytes(64))
+    with pytest.raises(rs.TooManyOriginalShards) as e:
+        enc.add_original_shard(bytes(64))
+    assert e.value == rs.TooManyOriginalShards(original_count=1)
+    with pytest.raises(rs.UnsupportedShardCount) as e:
+        E(0, 1, 64)
+    assert e.value == rs.UnsupportedShardCount(original_count=0, recovery_count=1)
+    with pytest.raises(rs.UnsupportedShardCount):
+        E(1, 1, 64).reset(0, 1, 64)
+
+
+@pytest.mark.parametrize("which", ["default", "high", "low"])
+def test_decoder_errors(rs, which):
+    D = {"default": rs.rate.DefaultRateDecoder, "high": rs.rate.HighRateDecoder, "low": rs.rate.LowRateDecoder}[which]
+    with pytest.raises(rs.DifferentShardSize) as e:
+        D(1, 1, 64).add_original_shard(0, bytes(128))
+    assert e.value == rs.DifferentShardSize(shard_bytes=64, got=128)
+    with pytest.raises(rs.DifferentShardSize):
+        D(1, 1, 64).add_recovery_shard(0, bytes(128))
+    d = D(1, 1, 64)
+    d.add_original_shard(0, bytes(64))
+    with pytest.raises(rs.DuplicateOriginalShardIndex) as e:
+        d.add_original_shard(0, bytes(64))
+    assert e.value == rs.DuplicateOriginalShardIndex(index=0)
+    d = D(1, 1, 64)
+    d.add_recovery_shard(0, bytes(64))
+    with pytest.raises(rs.DuplicateRecoveryShardIndex) as e:
+        d.add_recovery_shard(0, bytes(64))
+    assert e.value == rs.DuplicateRecoveryShardIndex(index=0)
+    with pytest.raises(rs.InvalidOriginalShardIndex) as e:
+        D(1, 1, 64).add_original_shard(1, bytes(64))
+    assert e.value == rs.InvalidOriginalShardIndex(original_count=1, index=1)
+    with pytest.raises(rs.InvalidRecoveryShardIndex) as e:
+        D(1, 1, 64).add_recovery_shard(1, bytes(64))
+    assert e.value == rs.InvalidRecoveryShardIndex(recovery_count=1, index=1)
+    with pytest.raises(rs.InvalidShardSize):
+        D(1, 1, 123)
+    with pytest.raises(rs.InvalidShardSize):
+        D(1, 1, 64).reset(1, 1, 123)
+    with pytest.raises(rs.NotEnoughShards) as e:
+        D(1, 1, 64).decode()
+    assert e.value == rs.NotEnoughShards(original_count=1, original_received_count=0, recovery_received_count=0)
+    with pytest.raises(rs.UnsupportedShardCount):
+        D(0, 1, 64)
+    with pytest.raises(rs.UnsupportedShardCount):
+        D(1, 1, 64).reset(0, 1, 64)
+
+
+def test_oneshot_errors(rs):
+    with pytest.raises(rs.DifferentShardSize) as e:
+        rs.encode(2, 1, [bytes(64), bytes(128)])
+    assert e.value == rs.DifferentShardSize(shard_bytes=64, got=128)
+    with pytest.raises(rs.InvalidShardSize):
+        rs.encode(1, 1, [b""])
+    with pytest.raises(rs.TooFewOriginalShards) as e:
+        rs.encode(1, 1, [])
+    assert e.value == rs.TooFewOriginalShards(original_count=1, original_received_count=0)
+    with pytest.raises(rs.TooManyOriginalShards):
+        rs.encode(1, 1, [bytes(64), bytes(64)])
+    with pytest.raises(rs.UnsupportedShardCount):
+        rs.encode(0, 1, [])
+    with pytest.raises(rs.UnsupportedShardCount):
+        rs.encode(1, 0, [bytes(64)])
+    assert rs.decode(1, 1, [(0, bytes(64))], []) == {}
+    with pytest.raises(rs.DifferentShardSize):
+        rs.decode(2, 1, [(0, bytes(64)), (1, bytes(128))], [(0, bytes(64))])
+    with pytest.raises(rs.DifferentShardSize):
+        rs.decode(1, 2, [(0, bytes(64))], [(0, bytes(64)), (1, bytes(128))])
+    with pytest.raises(rs.DifferentShardSize) as e:
+        rs.decode(1, 1, [(0, b"")], [(0, bytes(64))])
+    assert e.value == rs.DifferentShardSize(shard_bytes=64, got=0)
+    with pytest.raises(rs.DuplicateOriginalShardIndex):
+        rs.decode(2, 1, [(0, bytes(64)), (0, bytes(64))], [(0, bytes(64))])
+    with pytest.raises(rs.DuplicateRecoveryShardIndex):
+        rs.decode(1, 2, [(0, bytes(64))], [(0, bytes(64)), (0, bytes(64))])
+    with pytest.raises(rs.InvalidOriginalShardIndex):
+        rs.decode(1, 1, [(1, bytes(64))], [(0, bytes(64))])
+    with pytest.raises(rs.InvalidRecoveryShardIndex):
+        rs.decode(1, 1, [(0, bytes(64))], [(1, bytes(64))])
+    with pytest.raises(rs.InvalidShardSize):
+        rs.decode(1, 1, [(0, bytes(64))], [(0, b"")])
+    with pytest.raises(rs.NotEnoughShards):
+        rs.decode(1, 1, [], [])
+    with pytest.raises(rs.UnsupportedShardCount):
+        rs.decode(0, 1, [], [])
+    with pytest.raises(rs.UnsupportedShardCount):
+        rs.decode(1, 0, [], [])
+
+
+def test_encoder_result_and_size(rs):
+    """encoder_result.rs:122-172"""
+    orig = O.generate_original(2, 1024, 123)
+    enc = rs.ReedSolomonEncoder(2, 3, 1024)
+    for row in orig:
+        enc.add_original_shard(row.tobytes())
+    res = enc.encode()
+    allr = [res.recovery(0), res.recovery(1), res.recovery(2)]
+    assert res.recovery(3) is None
+    assert hashlib.sha256(b"".join(allr)).hexdigest() == [c for c in GOLD["single"] if c["name"] == "lib_roundtrip"][0][
+        "recovery_sha256"]
+
+
+def test_decoder_no_missing(rs):
+    """decoder_result.rs:209-238: all originals given -> empty result."""
+    orig = O.generate_original(3, 64, 0)
+    dec = rs.ReedSolomonDecoder(3, 2, 64)
+    for i in range(3):
+        dec.add_original_shard(i, orig[i].tobytes())
+    out = dec.decode()
+    assert len(out) == 0 and list(out.restored_original_iter()) == []
+
+
+# ---------------------------------------------------------------------------
+# Engine trait over device rows (src/engine.rs:234-291) vs the oracle
+
+@pytest.mark.parametrize("size,pos,delta,trunc,blocks", [(1, 0, 0, 1, 1), (2, 0, 5, 2, 2), (16, 3, 0, 16, 1),
+                                                         (256, 0, 256, 200, 3), (1024, 2, 1024, 1024, 2),
+                                                         (4096, 0, 4096, 4096, 1), (32768, 0, 0, 32768, 1)])
+@pytest.mark.parametrize("which", ["fft", "ifft"])
+def test_engine_transforms(torch, rs, size, pos, delta, trunc, blocks, which):
+    rng = np.random.default_rng(size + pos)
+    rows = pos + size + 1
+    x = rng.integers(0, 256, (rows, blocks * 64), dtype=np.uint8)
+    if which == "ifft":
+        x[pos + trunc:pos + size] = 0  # reference contract: zero past truncated_size
+    want = x.copy()
+    getattr(O.lib(), f"orc_{which}")(O.ptr(want), blocks, pos, size, trunc, delta)
+    d = _dev(torch, x)
+    getattr(rs.engine, which)(d, rows, blocks, pos, size, trunc, delta)
+    torch.cuda.synchronize()
+    got = d.cpu().numpy()
+    assert np.array_equal(got[pos:pos + trunc], want[pos:pos + trunc])
+    assert np.array_equal(got[:pos], x[:pos]) and np.array_equal(got[pos + size:], x[pos + size:])
+    if which == "ifft":
+        assert np.array_equal(got, want)
+
+
+def test_engine_mul_and_formal_derivative(torch, rs):
+    rng = np.random.default_rng(11)
+    x = rng.integers(0, 256, (5, 128), dtype=np.uint8)
+    for lm in (0, 1, 777, 65534, 65535):
+        want = x.copy()
+        O.lib().orc_mul(O.ptr(want), 10, lm)
+        d = _dev(torch, x)
+        rs.engine.mul(d, 10, lm)
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy(), want)
+    # utils.rs:99-104 is defined for power-of-two row counts only (it slices past
+    # the end otherwise); the device API rejects other counts
+    for n in (1, 2, 64, 1024):
+        x = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+        want = x.copy()
+        O.lib().orc_formal_derivative(O.ptr(want), 1, n)
+        d = _dev(torch, x)
+        rs.engine.formal_derivative(d, n, 1)
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy(), want)
+    with pytest.raises(ValueError):
+        rs.engine.formal_derivative(_dev(torch, np.zeros((3, 64), np.uint8)), 3, 1)
+
+
+# ---------------------------------------------------------------------------
+# BASELINE.json configurations at full size: properties + column samples
+
+def _column_sample_check(orig, got, M, rate, blocks=(0, 7, -1)):
+    S = orig.shape[1]
+    nb = S // 64
+    for b in blocks:
+        b %= nb
+        cols = slice(64 * b, 64 * b + 64)
+        want = O.encode(rate, np.ascontiguousarray(orig[:, cols]), M)
+        assert np.array_equal(got[:, cols], want), f"column block {b}"
+
+
+@pytest.mark.parametrize("N,M,S", [(1024, 1024, 1024), (32768, 32768, 1024)])
+def test_baseline_encode_configs(torch, rs, N, M, S):
+    orig = O.generate_original(N, S, 0)
+    got = gpu_encode(torch, rs, "default", orig, M)
+    _column_sample_check(orig, got, M, "default")
+    if N * S <= (64 << 20):
+        O.lib().orc_select_engine(1)
+        try:
+            assert np.array_equal(got, O.encode("default", orig, M))
+        finally:
+            O.lib().orc_select_engine(0)
+
+
+@pytest.mark.parametrize("loss", [0.01, 1.0])
+def test_baseline_decode_8192_64k(torch, rs, loss):
+    """config 4: 8192:8192 x 64 KiB, decode at 1% and 100% loss (benchmarks.rs:113-138 pattern)."""
+    N = M = 8192
+    S = 65536
+    orig = np.random.default_rng(1).integers(0, 256, (N, S), dtype=np.uint8)
+    d_orig = _dev(torch, orig)
+    d_rec = torch.empty((M, S), dtype=torch.uint8, device="cuda")
+    rs.encode_device(N, M, S, d_orig, d_rec)
+    torch.cuda.synchronize()
+    rec_cols = d_rec[:, :128].cpu().numpy()
+    assert np.array_equal(rec_cols, O.encode("default", np.ascontiguousarray(orig[:, :128]), M))
+    L = -(-min(N, M) * int(loss * 100) // 100)
+    op = np.ones(N, np.uint8)
+    op[N - L:] = 0
+    rp = np.zeros(M, np.uint8)
+    rp[:L] = 1
+    d_out = torch.zeros_like(d_orig)
+    d_in = d_orig.clone()
+    d_in[N - L:] = 0
+    rs.decode_device(N, M, S, d_in, op, d_rec, rp, d_out)
+    torch.cuda.synchronize()
+    assert torch.equal(d_out[N - L:], d_orig[N - L:])
