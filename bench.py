@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident Reed-Solomon GF(2^16) encode/decode on MI355X.
+
+Metric (BASELINE.json): GiB/s of (original + recovery) bytes, device-resident,
+at 1024:1024 x 1024 B shards (BASELINE.json configs[1]).  A "step" is one
+encode of one 1024:1024 x 1 KiB stripe whose shards already sit in HBM
+(rs_encode_device through the C ABI).  Decode at 1 % and 100 % loss
+(loss pattern of the reference's benches/benchmarks.rs:113-138) is timed the
+same way and reported beside the headline value.
+
+N > 1 (torchrun, one process per GPU): every rank encodes its own stripes
+(independent objects, no data-path collective) -> "scaling": "weak"; value =
+bytes of all ranks / max-over-ranks time.
+
+roofline: per-kernel HIP-event timing of the launches of the timed workload
+(rs_profile_enable), dominant kernel = largest total time; achieved = its
+algorithmic bytes per launch / its average duration; peak = 8 TB/s HBM3E.
+cpu_baseline: the reference's AVX2 algorithm restated in C (oracle/avx2_port.c),
+single thread, on a bounded sample, rank 0 at N = 1 only.
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "reed-solomon-simd_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+METRIC = "GiB/s (original+recovery) encode & decode, device-resident, 1024:1024×1024B"
+HBM_PEAK_GBS = 8000.0
+
+CONFIGS = {
+    # name: (original_count, recovery_count, shard_bytes)
+    "1024x1024x1k": (1024, 1024, 1024),        # configs[1] (the metric's config)
+    "32768x32768x1k": (32768, 32768, 1024),    # configs[2]
+    "8192x8192x64k": (8192, 8192, 65536),      # configs[3] (decode)
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--config", default="1024x1024x1k", choices=sorted(CONFIGS))
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-decode", action="store_true")
+    p.add_argument("--profile-steps", type=int, default=50)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    import reed_solomon_simd as rs
+
+    ctx = rs.Context(local)
+    N, M, S = CONFIGS[args.config]
+    dev = torch.device("cuda", local)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    d_orig = torch.randint(0, 256, (N, S), dtype=torch.uint8, device=dev, generator=g)
+    d_rec = torch.empty((M, S), dtype=torch.uint8, device=dev)
+    d_out = torch.empty((N, S), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.Stream(device=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(fn, steps, warmup):
+        with torch.cuda.stream(stream):
+            for _ in range(warmup):
+                fn()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        with torch.cuda.stream(stream):
+            ev0.record(stream)
+            for _ in range(steps):
+                fn()
+            ev1.record(stream)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        barrier()
+        return max_over_ranks(wall), max_over_ranks(ev0.elapsed_time(ev1) / 1e3)
+
+    def enc():
+        rs.encode_device(N, M, S, d_orig, d_rec, stream=stream, ctx=ctx)
+
+    # ---- headline: encode -------------------------------------------------
+    wall, gpu_t = timed(enc, args.steps, args.warmup)
+    step_bytes = (N + M) * S
+    value = step_bytes * args.steps * world / wall / 2**30
+
+    # ---- per-kernel timing of the same workload ----------------------------
+    rs.profile_enable(True, ctx=ctx)
+    with torch.cuda.stream(stream):
+        for _ in range(args.profile_steps):
+            enc()
+    torch.cuda.synchronize()
+    recs = rs.profile_collect(ctx)
+    rs.profile_enable(False, ctx=ctx)
+    agg = {}
+    for name, ms, by in recs:
+        a = agg.setdefault(name, [0.0, 0, 0])
+        a[0] += ms
+        a[1] += 1
+        a[2] += by
+    kernels = {k: {"launches_per_step": v[1] / args.profile_steps, "avg_us": 1e3 * v[0] / v[1],
+                   "bytes_per_launch": v[2] // v[1]} for k, v in agg.items()}
+    dom = max(agg, key=lambda k: agg[k][0])
+    dom_avg_s = agg[dom][0] / agg[dom][1] / 1e3
+    achieved = kernels[dom]["bytes_per_launch"] / dom_avg_s / 1e9
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "bytes_per_launch": kernels[dom]["bytes_per_launch"], "avg_us": round(dom_avg_s * 1e6, 3),
+                "kernels": kernels}
+
+    # ---- decode at 1 % and 100 % loss (benchmarks.rs:113-138) --------------
+    decode = {}
+    if not args.no_decode:
+        for pct in (1, 100):
+            L = -(-min(N, M) * pct // 100)
+            op = rs.present_mask([1] * (N - L) + [0] * L)
+            rp = rs.present_mask([1] * L + [0] * (M - L))
+
+            def dec(op=op, rp=rp):
+                rs.decode_device(N, M, S, d_orig, op, d_rec, rp, d_out, stream=stream, ctx=ctx)
+
+            w, _ = timed(dec, args.steps, args.warmup)
+            decode[f"{pct}pct"] = round(step_bytes * args.steps * world / w / 2**30, 3)
+
+    # ---- CPU baseline (rank 0, N = 1 only) ----------------------------------
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 5), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (uniform random bytes)",
+            "config": {"workload": f"encode {N}:{M} x {S} B, device-resident (rs_encode_device)",
+                       "original_count": N, "recovery_count": M, "shard_bytes": S,
+                       "rate": "high" if rs.use_high_rate(N, M) == 1 else "low",
+                       "parallelism": f"replicas x{world} (independent stripes)"},
+            "gpu_event_ms_per_step": round(gpu_t / args.steps * 1e3, 5),
+            "decode_GiBps": decode,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(seconds):
+    """AVX2 restatement of the reference engine, 1 thread, 1024:1024 x 1 KiB encode."""
+    import numpy as np
+    import oracle_lib as O
+
+    if O.lib().orc_select_engine(1) != 0:
+        return {"value": None, "unit": "GiB/s", "cores": 1, "kind": "port", "sample": "AVX2 unavailable on host"}
+    orig = np.random.default_rng(0).integers(0, 256, (1024, 1024), dtype=np.uint8)
+    O.encode("default", orig, 1024)
+    it, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        O.encode("default", orig, 1024)
+        it += 1
+    dt = time.perf_counter() - t0
+    O.lib().orc_select_engine(0)
+    return {"value": round(2 * 1024 * 1024 * it / dt / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{it} encodes of 1024:1024 x 1024 B in {dt:.1f} s (shard copy-in + encode, like "
+                      f"benches/benchmarks.rs:101-107), single thread, {platform.processor() or platform.machine()}"}
+
+
+if __name__ == "__main__":
+    main()

@@ -176,6 +176,16 @@ void rs_engine_eval_poly(uint16_t *erasures, uint64_t truncated_size);
 rs_status rs_engine_formal_derivative(rs_context *ctx, void *d_rows, uint64_t shard_count, uint64_t shard_len_64,
                                       void *stream);
 
+/* ---- kernel timing (bench instrumentation, not a reference item) ----
+ * While enabled, every kernel the context launches is bracketed by HIP events
+ * on the stream it is launched on.  rs_profile_collect synchronizes those
+ * events and returns, in launch order, each launch's duration (ms), its
+ * kernel name and the algorithmic HBM bytes of that launch (rows it must read
+ * from memory + rows it writes, times the row size); then clears the record.
+ * Returns the number of records written (<= max). */
+rs_status rs_profile_enable(rs_context *ctx, int enable);
+int rs_profile_collect(rs_context *ctx, float *ms, uint64_t *bytes, const char **names, int max);
+
 /* ---- GF(2^16) tables (src/engine/tables.rs), host copies ---- */
 const uint16_t *rs_table_exp(void);       /* 65536 */
 const uint16_t *rs_table_log(void);       /* 65536 */

@@ -105,7 +105,7 @@ struct DevBuf {
 };
 
 struct Workspace {
-    DevBuf work, work2, rowinfo, state;
+    DevBuf buf[4], rowinfo, state;
     std::vector<uint8_t> h_state;
 };
 
@@ -120,7 +120,44 @@ struct rs_context {
     uint16_t lw0 = 0;
     std::mutex mu;  // guards ws (device-resident API scratch)
     Workspace ws;
+    // kernel timing (rs_profile_enable)
+    bool prof = false;
+    struct Rec {
+        hipEvent_t a, b;
+        std::string name;
+        uint64_t bytes;
+    };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    hipEvent_t take_event() {
+        if (pool.empty()) {
+            hipEvent_t e;
+            check(hipEventCreate(&e));
+            return e;
+        }
+        hipEvent_t e = pool.back();
+        pool.pop_back();
+        return e;
+    }
 };
+
+namespace {
+// Kernel timing (rs_profile_enable): the context of the current API call.
+thread_local rs_context *t_prof_ctx = nullptr;
+struct ProfScope {
+    explicit ProfScope(rs_context *c) { t_prof_ctx = c && c->prof ? c : nullptr; }
+    ~ProfScope() { t_prof_ctx = nullptr; }
+};
+void prof_begin(hipStream_t s, hipEvent_t *ev) {
+    *ev = t_prof_ctx->take_event();
+    check(hipEventRecord(*ev, s));
+}
+void prof_end(hipStream_t s, hipEvent_t ev, const char *name, uint64_t bytes) {
+    hipEvent_t b = t_prof_ctx->take_event();
+    check(hipEventRecord(b, s));
+    t_prof_ctx->recs.push_back({ev, b, name, bytes});
+}
+}  // namespace
 
 namespace {
 
@@ -141,103 +178,162 @@ rs::PassArgs base_args(rs_context *ctx, const Geom &g, uint32_t n) {
     return A;
 }
 
-// split of a 2^L transform into passes: L <= 8 -> single; else low bits [0,a)
-// in passes A/C, high bits [a, L) in the fused pass B.
-struct Split {
-    bool single;
-    uint32_t L, a, kb;
+// Split of a 2^L-row transform into bit levels of at most kMaxK bits each,
+// low to high: level k covers transform-row bits [lo_k, lo_k + K_k).  The
+// IFFT runs levels 0..m-1 ascending, the FFT m-1..0 descending; the top
+// level's IFFT + FFT are fused into one pass (DESIGN.md "Pass structure").
+constexpr uint32_t kMaxK = 6;
+struct Levels {
+    uint32_t m = 0;
+    uint32_t lo[4] = {0, 0, 0, 0}, K[4] = {0, 0, 0, 0};
 };
-Split split(uint32_t L) {
-    if (L <= 8) return {true, L, 0, L};
-    const uint32_t a = (L + 1) / 2;
-    return {false, L, a, L - a};
+Levels levels(uint32_t L) {
+    Levels v;
+    v.m = L == 0 ? 1 : (L + kMaxK - 1) / kMaxK;
+    // the fused top level does two transforms: give it the smallest share
+    uint32_t rest = L;
+    for (uint32_t k = 0; k < v.m; ++k) {
+        const uint32_t left = v.m - k;
+        v.K[k] = (rest + left - 1) / left;
+        v.lo[k] = L - rest;
+        rest -= v.K[k];
+    }
+    return v;
 }
 
-void launch(int K, int flags, rs::PassArgs A, uint32_t nsets, uint32_t a, hipStream_t s) {
+// Algorithmic HBM bytes of one pass: rows it must read + rows it writes.
+uint64_t pass_bytes(int K, const rs::PassArgs &A, uint64_t decode_rows_read, uint64_t decode_rows_written) {
+    const uint64_t span = uint64_t(A.n) * (A.grid_chunks + A.in_chunks + A.out_chunks - 2);
+    uint64_t rd = 0, wr = 0;
+    if (A.work_in) rd = (uint64_t(A.nsets) << K) * A.grid_chunks * A.in_chunks;
+    else if (decode_rows_read) rd = decode_rows_read;
+    else
+        for (uint32_t k = 0; k < A.nsrc; ++k)
+            rd += std::min<uint64_t>(A.src[k].row_end, span) - std::min<uint64_t>(A.src[k].row_begin, span);
+    if (A.xor_in) rd += uint64_t(A.nsets) << K;
+    if (A.work_out) wr = (uint64_t(A.nsets) << K) * A.grid_chunks * A.out_chunks;
+    else if (decode_rows_written) wr = decode_rows_written;
+    else wr = std::min<uint64_t>(A.dst.row_end, span) - std::min<uint64_t>(A.dst.row_begin, span);
+    const uint64_t row = uint64_t(A.packs) * 8;
+    return (rd + wr) * row;
+}
+
+void launch(int K, int flags, rs::PassArgs A, uint32_t nsets, uint32_t a, hipStream_t s, uint64_t dec_rd = 0,
+            uint64_t dec_wr = 0) {
     A.nsets = nsets;
     A.a = a;
+    hipEvent_t ev = nullptr;
+    if (t_prof_ctx) prof_begin(s, &ev);
     check(rs::launch_pass(K, flags, A, s));
+    if (t_prof_ctx) {
+        static const char *names[4] = {"k_pass_copy", "k_pass_ifft", "k_pass_fft", "k_pass_ifft_fft"};
+        static thread_local char buf[64];
+        snprintf(buf, sizeof buf, "%s<K=%d>", names[flags & 3], K);
+        prof_end(s, ev, buf, pass_bytes(K, A, dec_rd, dec_wr));
+    }
 }
 
-// HighRate encode (rate_high.rs:44-87) from device rows to device rows.
+// One pass over bit level k of a 2^L-row transform (n rows per chunk).
+void run_level(rs::PassArgs A, const Levels &lv, uint32_t k, int flags, uint32_t n, hipStream_t s,
+               uint64_t dec_rd = 0, uint64_t dec_wr = 0) {
+    launch(lv.K[k], flags, A, n >> lv.K[k], lv.lo[k], s, dec_rd, dec_wr);
+}
+
+// HighRate encode (rate_high.rs:44-87) from device rows to device rows:
+// chunk c's IFFT uses skew_delta c*n + n, the chunks are XOR-folded, one FFT
+// with skew_delta 0 produces the recovery rows.
 void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint64_t M, const uint8_t *orig,
                  uint8_t *rec, hipStream_t s) {
     const uint32_t n = uint32_t(next_pow2(M)), L = ilog2(n);
     const uint32_t C = uint32_t((N + n - 1) / n);
-    const Split sp = split(L);
+    const Levels lv = levels(L);
     rs::PassArgs A = base_args(ctx, g, n);
     A.ifft_delta = n;
     A.ifft_delta_step = n;
-    if (sp.single) {
-        A.src[0] = {orig, g.stride, 0, uint32_t(N)};
+    const rs::RowMap src{orig, g.stride, 0, uint32_t(N)}, dst{rec, g.stride, 0, uint32_t(M)};
+    if (lv.m == 1) {
+        A.src[0] = src;
         A.nsrc = 1;
         A.in_chunks = C;
-        A.dst = {rec, g.stride, 0, uint32_t(M)};
-        launch(L, rs::kIfft | rs::kFft, A, 1, 0, s);
+        A.dst = dst;
+        run_level(A, lv, 0, rs::kIfft | rs::kFft, n, s);
         return;
     }
-    uint8_t *W = static_cast<uint8_t *>(ws.work.get(size_t(C) * n * g.stride));
-    rs::PassArgs P1 = A;  // IFFT low bits, per chunk
-    P1.src[0] = {orig, g.stride, 0, uint32_t(N)};
-    P1.nsrc = 1;
-    P1.grid_chunks = C;
-    P1.work_out = W;
-    P1.work_stride = g.stride;
-    launch(sp.a, rs::kIfft, P1, n >> sp.a, 0, s);
-    rs::PassArgs P2 = A;  // IFFT high bits per chunk, XOR-fold, FFT high bits
-    P2.work_in = W;
-    P2.work_stride = g.stride;
-    P2.in_chunks = C;
-    P2.work_out = W;
-    launch(sp.kb, rs::kIfft | rs::kFft, P2, 1u << sp.a, sp.a, s);
-    rs::PassArgs P3 = A;  // FFT low bits -> recovery rows
-    P3.work_in = W;
-    P3.work_stride = g.stride;
-    P3.dst = {rec, g.stride, 0, uint32_t(M)};
-    launch(sp.a, rs::kFft, P3, n >> sp.a, 0, s);
+    uint8_t *W = static_cast<uint8_t *>(ws.buf[0].get(size_t(C) * n * g.stride));
+    A.work_stride = g.stride;
+    for (uint32_t k = 0; k + 1 < lv.m; ++k) {  // IFFT, low levels, every chunk
+        rs::PassArgs P = A;
+        P.grid_chunks = C;
+        if (k == 0) P.src[0] = src, P.nsrc = 1;
+        else P.work_in = W;
+        P.work_out = W;
+        run_level(P, lv, k, rs::kIfft, n, s);
+    }
+    rs::PassArgs T = A;  // top level: IFFT per chunk, XOR-fold, FFT
+    T.work_in = W;
+    T.in_chunks = C;
+    T.work_out = W;
+    run_level(T, lv, lv.m - 1, rs::kIfft | rs::kFft, n, s);
+    for (int k = int(lv.m) - 2; k >= 0; --k) {  // FFT, low levels
+        rs::PassArgs P = A;
+        P.work_in = W;
+        if (k == 0) P.dst = dst;
+        else P.work_out = W;
+        run_level(P, lv, k, rs::kFft, n, s);
+    }
 }
 
-// LowRate encode (rate_low.rs:44-87).
+// LowRate encode (rate_low.rs:44-87): one IFFT (skew 0), then output chunk c
+// is FFT'd with skew_delta c*n + n.
 void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint64_t M, const uint8_t *orig,
                 uint8_t *rec, hipStream_t s) {
     const uint32_t n = uint32_t(next_pow2(N)), L = ilog2(n);
     const uint32_t C = uint32_t((M + n - 1) / n);
-    const Split sp = split(L);
+    const Levels lv = levels(L);
     rs::PassArgs A = base_args(ctx, g, n);
     A.fft_delta = n;
     A.fft_delta_step = n;
-    if (sp.single) {
-        A.src[0] = {orig, g.stride, 0, uint32_t(N)};
+    const rs::RowMap src{orig, g.stride, 0, uint32_t(N)}, dst{rec, g.stride, 0, uint32_t(M)};
+    if (lv.m == 1) {
+        A.src[0] = src;
         A.nsrc = 1;
         A.out_chunks = C;
-        A.dst = {rec, g.stride, 0, uint32_t(M)};
-        launch(L, rs::kIfft | rs::kFft, A, 1, 0, s);
+        A.dst = dst;
+        run_level(A, lv, 0, rs::kIfft | rs::kFft, n, s);
         return;
     }
-    uint8_t *W = static_cast<uint8_t *>(ws.work.get(size_t(n) * g.stride));
-    uint8_t *W2 = static_cast<uint8_t *>(ws.work2.get(size_t(C) * n * g.stride));
-    rs::PassArgs P1 = A;
-    P1.src[0] = {orig, g.stride, 0, uint32_t(N)};
-    P1.nsrc = 1;
-    P1.work_out = W;
-    P1.work_stride = g.stride;
-    launch(sp.a, rs::kIfft, P1, n >> sp.a, 0, s);
-    rs::PassArgs P2 = A;
-    P2.work_in = W;
-    P2.work_stride = g.stride;
-    P2.out_chunks = C;
-    P2.work_out = W2;
-    launch(sp.kb, rs::kIfft | rs::kFft, P2, 1u << sp.a, sp.a, s);
-    rs::PassArgs P3 = A;
-    P3.work_in = W2;
-    P3.work_stride = g.stride;
-    P3.grid_chunks = C;
-    P3.dst = {rec, g.stride, 0, uint32_t(M)};
-    launch(sp.a, rs::kFft, P3, n >> sp.a, 0, s);
+    uint8_t *W = static_cast<uint8_t *>(ws.buf[0].get(size_t(n) * g.stride));
+    uint8_t *W2 = static_cast<uint8_t *>(ws.buf[1].get(size_t(C) * n * g.stride));
+    A.work_stride = g.stride;
+    for (uint32_t k = 0; k + 1 < lv.m; ++k) {
+        rs::PassArgs P = A;
+        if (k == 0) P.src[0] = src, P.nsrc = 1;
+        else P.work_in = W;
+        P.work_out = W;
+        run_level(P, lv, k, rs::kIfft, n, s);
+    }
+    rs::PassArgs T = A;  // top level: IFFT, then FFT once per output chunk
+    T.work_in = W;
+    T.out_chunks = C;
+    T.work_out = W2;
+    run_level(T, lv, lv.m - 1, rs::kIfft | rs::kFft, n, s);
+    for (int k = int(lv.m) - 2; k >= 0; --k) {
+        rs::PassArgs P = A;
+        P.grid_chunks = C;
+        P.work_in = W2;
+        if (k == 0) P.dst = dst;
+        else P.work_out = W2;
+        run_level(P, lv, k, rs::kFft, n, s);
+    }
 }
 
 // Decode (rate_high.rs:172-254 / rate_low.rs:172-254).  Only missing original
 // rows of `restored` are written.
+//
+// Multi-level formal derivative (DESIGN.md "Formal derivative across passes"):
+// with X_k the IFFT output after levels 0..k and P_(k) the derivative terms of
+// level k's bits,  U = F_top(P_(top) X_top),  V_{m-2} = F_{m-2}((I + P_(m-2)) X_{m-2} + U),
+// V_k = F_k(P_(k) X_k + V_{k+1}) for k < m-2, and V_0 is FFT(derivative(IFFT)).
 void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64_t N, uint64_t M,
                 const uint8_t *orig, const uint8_t *orig_present, const uint8_t *rec, const uint8_t *rec_present,
                 uint8_t *restored, hipStream_t s) {
@@ -255,18 +351,24 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
         for (uint32_t r = 0; r < N; ++r) st[r] = orig_present[r] ? 2 : 1;
         for (uint32_t r = chunk; r < end; ++r) st[r] = rec_present[r - chunk] ? 2 : 1;
     }
+    uint64_t received = 0, missing = 0;
+    for (uint32_t r = 0; r < nd; ++r) received += st[r] == 2;
+    for (uint64_t i = 0; i < N; ++i) missing += !orig_present[i];
     uint8_t *d_state = static_cast<uint8_t *>(ws.state.get(nd));
     uint32_t *d_rowinfo = static_cast<uint32_t *>(ws.rowinfo.get(size_t(nd) * 4));
     check(hipMemcpyAsync(d_state, st.data(), nd, hipMemcpyHostToDevice, s));
+    hipEvent_t ev = nullptr;
+    if (t_prof_ctx) prof_begin(s, &ev);
     check(rs::launch_eval_poly(u, !high, end, d_state, ctx->d_lwfold + (nd - 1), ctx->lw0, d_rowinfo, s));
+    if (t_prof_ctx) prof_end(s, ev, "k_eval_poly", uint64_t(nd) * 5);
 
     rs::PassArgs A = base_args(ctx, g, nd);
     A.rowinfo = d_rowinfo;
     const rs::RowMap rec_map{rec, g.stride, high ? 0u : chunk, high ? uint32_t(M) : end};
     const rs::RowMap orig_map{orig, g.stride, high ? chunk : 0u, high ? end : uint32_t(N)};
     const rs::RowMap out_map{restored, g.stride, orig_map.row_begin, orig_map.row_end};
-    const Split sp = split(u);
-    if (sp.single) {
+    const Levels lv = levels(u);
+    if (lv.m == 1) {
         A.src[0] = rec_map;
         A.src[1] = orig_map;
         A.nsrc = 2;
@@ -274,33 +376,44 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
         A.fd_mode = 2;
         A.dst = out_map;
         A.reveal = 1;
-        launch(u, rs::kIfft | rs::kFft, A, 1, 0, s);
+        run_level(A, lv, 0, rs::kIfft | rs::kFft, nd, s, received, missing);
         return;
     }
-    uint8_t *W = static_cast<uint8_t *>(ws.work.get(size_t(nd) * g.stride));
-    uint8_t *Z = static_cast<uint8_t *>(ws.work2.get(size_t(nd) * g.stride));
-    rs::PassArgs P1 = A;  // scale received rows, IFFT low bits -> W
-    P1.src[0] = rec_map;
-    P1.src[1] = orig_map;
-    P1.nsrc = 2;
-    P1.load_scale = 1;
-    P1.work_out = W;
-    P1.work_stride = g.stride;
-    launch(sp.a, rs::kIfft, P1, nd >> sp.a, 0, s);
-    rs::PassArgs P2 = A;  // IFFT high, H-part of the derivative, FFT high -> Z
-    P2.work_in = W;
-    P2.work_stride = g.stride;
-    P2.fd_mode = 1;
-    P2.work_out = Z;
-    launch(sp.kb, rs::kIfft | rs::kFft, P2, 1u << sp.a, sp.a, s);
-    rs::PassArgs P3 = A;  // (I + Lo) W ^ Z, FFT low, reveal missing originals
-    P3.work_in = W;
-    P3.work_stride = g.stride;
-    P3.fd_mode = 2;
-    P3.xor_in = Z;
-    P3.dst = out_map;
-    P3.reveal = 1;
-    launch(sp.a, rs::kFft, P3, nd >> sp.a, 0, s);
+    uint8_t *X[3];
+    for (uint32_t k = 0; k + 1 < lv.m; ++k) X[k] = static_cast<uint8_t *>(ws.buf[k].get(size_t(nd) * g.stride));
+    uint8_t *U = static_cast<uint8_t *>(ws.buf[3].get(size_t(nd) * g.stride));
+    A.work_stride = g.stride;
+    for (uint32_t k = 0; k + 1 < lv.m; ++k) {  // scale received rows (level 0), IFFT low levels
+        rs::PassArgs P = A;
+        if (k == 0) {
+            P.src[0] = rec_map;
+            P.src[1] = orig_map;
+            P.nsrc = 2;
+            P.load_scale = 1;
+        } else {
+            P.work_in = X[k - 1];
+        }
+        P.work_out = X[k];
+        run_level(P, lv, k, rs::kIfft, nd, s, k == 0 ? received : 0, 0);
+    }
+    rs::PassArgs T = A;  // top: IFFT, its derivative terms, FFT -> U
+    T.work_in = X[lv.m - 2];
+    T.fd_mode = 1;
+    T.work_out = U;
+    run_level(T, lv, lv.m - 1, rs::kIfft | rs::kFft, nd, s);
+    for (int k = int(lv.m) - 2; k >= 0; --k) {  // V_k, last one revealed
+        rs::PassArgs P = A;
+        P.work_in = X[k];
+        P.fd_mode = k == int(lv.m) - 2 ? 2 : 1;
+        P.xor_in = U;
+        if (k == 0) {
+            P.dst = out_map;
+            P.reveal = 1;
+        } else {
+            P.work_out = U;
+        }
+        run_level(P, lv, k, rs::kFft, nd, s, 0, k == 0 ? missing : 0);
+    }
 }
 
 const char *hip_msg(hipError_t e) { return hipGetErrorString(e); }
@@ -487,6 +600,7 @@ rs_status rs_encode_device(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M
     if (S % 64) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     return guarded(err, [&]() -> rs_status {
         std::lock_guard<std::mutex> lock(ctx->mu);
+        ProfScope prof(ctx);
         const Geom g{S, uint32_t(S / 8)};
         auto s = static_cast<hipStream_t>(stream);
         if (high)
@@ -516,6 +630,7 @@ rs_status rs_decode_device(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M
     if (have_o == N) return set_err(err, RS_OK);
     return guarded(err, [&]() -> rs_status {
         std::lock_guard<std::mutex> lock(ctx->mu);
+        ProfScope prof(ctx);
         const Geom g{S, uint32_t(S / 8)};
         decode_dev(ctx, ctx->ws, high, g, N, M, static_cast<const uint8_t *>(d_orig), orig_present,
                    static_cast<const uint8_t *>(d_rec), rec_present, static_cast<uint8_t *>(d_restored),
@@ -793,23 +908,13 @@ static rs_status engine_xform(rs_context *ctx, void *rows, uint64_t count, uint6
         const uint32_t n = uint32_t(size), L = ilog2(n);
         rs::PassArgs A = base_args(ctx, g, n);
         A.ifft_delta = A.fft_delta = uint32_t(delta);
-        const Split sp = split(L);
-        const int flag = fft ? rs::kFft : rs::kIfft;
-        if (sp.single) {
-            A.work_in = A.work_out = base;
-            A.work_stride = g.stride;
-            launch(L, flag, A, 1, 0, s);
-            return RS_OK;
-        }
-        // two passes, in place: FFT = high bits then low bits; IFFT = low then high
+        const Levels lv = levels(L);
         A.work_in = A.work_out = base;
         A.work_stride = g.stride;
-        if (fft) {
-            launch(sp.kb, flag, A, 1u << sp.a, sp.a, s);
-            launch(sp.a, flag, A, n >> sp.a, 0, s);
-        } else {
-            launch(sp.a, flag, A, n >> sp.a, 0, s);
-            launch(sp.kb, flag, A, 1u << sp.a, sp.a, s);
+        // in place: IFFT runs levels low -> high, FFT high -> low
+        for (uint32_t i = 0; i < lv.m; ++i) {
+            const uint32_t k = fft ? lv.m - 1 - i : i;
+            run_level(A, lv, k, fft ? rs::kFft : rs::kIfft, n, s);
         }
         return RS_OK;
     });
@@ -840,12 +945,43 @@ rs_status rs_engine_formal_derivative(rs_context *ctx, void *d_rows, uint64_t co
     return guarded(nullptr, [&]() -> rs_status {
         std::lock_guard<std::mutex> lock(ctx->mu);
         const uint64_t bytes = count * len64 * 64;
-        auto *tmp = static_cast<uint8_t *>(ctx->ws.work.get(bytes));
+        auto *tmp = static_cast<uint8_t *>(ctx->ws.buf[0].get(bytes));
         auto s = static_cast<hipStream_t>(stream);
         check(hipMemcpyAsync(tmp, d_rows, bytes, hipMemcpyDeviceToDevice, s));
         check(rs::launch_formal_derivative(tmp, static_cast<uint8_t *>(d_rows), uint32_t(count), len64 * 64, s));
         return RS_OK;
     });
+}
+
+rs_status rs_profile_enable(rs_context *ctx, int enable) {
+    if (!ctx) return RS_ERR_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    ctx->prof = enable != 0;
+    return RS_OK;
+}
+
+int rs_profile_collect(rs_context *ctx, float *ms, uint64_t *bytes, const char **names, int max) {
+    if (!ctx) return -1;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    static thread_local std::vector<std::string> keep;
+    keep.clear();
+    int n = 0;
+    for (auto &r : ctx->recs) {
+        if (n < max) {
+            float t = 0;
+            if (hipEventSynchronize(r.b) == hipSuccess) (void)hipEventElapsedTime(&t, r.a, r.b);
+            if (ms) ms[n] = t;
+            if (bytes) bytes[n] = r.bytes;
+            keep.push_back(r.name);
+            ++n;
+        }
+        ctx->pool.push_back(r.a);
+        ctx->pool.push_back(r.b);
+    }
+    if (names)
+        for (int i = 0; i < n; ++i) names[i] = keep[i].c_str();
+    ctx->recs.clear();
+    return n;
 }
 
 void rs_engine_eval_poly(uint16_t *erasures, uint64_t truncated_size) { rs::eval_poly_host(erasures, truncated_size); }

@@ -54,7 +54,17 @@ struct PassArgs {
     const uint32_t *lut = nullptr;      // perm tables indexed by log factor
 };
 
-enum PassFlags { kIfft = 1, kFft = 2 };
+enum PassFlags {
+    kIfft = 1,
+    kFft = 2,
+    // derived from PassArgs by launch_pass (compile-time kernel variants):
+    kMultiIn = 4,
+    kMultiOut = 8,
+    kScale = 16,
+    kFd = 32,
+    kXorIn = 64,
+    kReveal = 128
+};
 
 // Launch one pass on `stream`.  K = log2(rows per set).
 hipError_t launch_pass(int K, int flags, const PassArgs &args, hipStream_t stream);

@@ -93,9 +93,11 @@ struct Pass {
 
     template <bool PB>
     static __device__ __forceinline__ uint32_t lrow(uint32_t w, int i) {
+        // '+' (not '|': the bits are disjoint) lets the compiler fold the
+        // register index into LDS / global immediate offsets
         if constexpr (W == 1) return i;
-        if constexpr (PB) return (uint32_t(i) << (K - LR)) | w;
-        return (w << LR) | uint32_t(i);
+        if constexpr (PB) return (uint32_t(i) << (K - LR)) + w;
+        return (w << LR) + uint32_t(i);
     }
 };
 
@@ -105,53 +107,117 @@ struct Ctx {
     __device__ __forceinline__ uint32_t grow(uint32_t j, int K) const { return s_lo + (j << a) + (s_hi << (a + K)); }
 };
 
-template <int K, int LR, bool PB>
-__device__ __forceinline__ void load_rows(const PassArgs &A, const Ctx &c, uint32_t chunk, uint32_t (&lo)[1 << LR],
-                                          uint32_t (&hi)[1 << LR]) {
+// LDS layout (dynamic, 16-byte aligned), in 32-bit words:
+//   plane : 64 lanes x 2^K rows, one data plane (low or high words) at a time
+//   tab   : 2^K tables x 20 words -- the twiddle tables of the transform in
+//           flight (slot = 2^K - 2^(K-b) + group, b = local layer), or the
+//           per-row scale tables of a decode load / reveal
+//   rinfo : 2^K words -- decode row info of the set's rows
+template <int K>
+struct Lds {
+    static constexpr uint32_t kPlane = uint32_t(kLanes) << K;
+    static constexpr uint32_t kTab = 20u << K;
+    static constexpr uint32_t kRows = 1u << K;
+    static constexpr size_t bytes() { return size_t(kPlane + kTab + kRows) * 4; }
+};
+
+// slot of the twiddle table of local layer b for local row j (bit b of j clear)
+template <int K>
+__device__ __forceinline__ uint32_t tw_slot(int b, uint32_t j) {
+    return (1u << K) - (1u << (K - b)) + (j >> (b + 1));
+}
+
+// Stage the 2^K - 1 twiddle tables of this set for one transform into LDS.
+template <int K>
+__device__ __forceinline__ void stage_twiddles(const PassArgs &A, const Ctx &c, uint32_t delta, uint32_t *tab) {
+    constexpr uint32_t slots = (1u << K) - 1;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < slots * 20; t += blockDim.x) {
+        const uint32_t slot = t / 20, word = t - slot * 20;
+        const uint32_t y = (1u << K) - slot;                  // in [2, 2^K]
+        const int b = K - (32 - __builtin_clz(y - 1));        // K - ceil(log2 y)
+        const uint32_t g = slot - ((1u << K) - (1u << (K - b)));
+        const uint32_t row = c.grow(g << (b + 1), K);
+        const uint32_t gb = c.a + b;
+        const uint32_t idx = (row & ~((2u << gb) - 1u)) + (1u << gb) + delta - 1u;
+        tab[t] = A.tw[idx * 20u + word];
+    }
+    __syncthreads();
+}
+
+// Stage per-row decode info and scale tables (load: factor, reveal: 65535 - factor).
+template <int K>
+__device__ __forceinline__ void stage_rows(const PassArgs &A, const Ctx &c, uint32_t chunk, bool reveal,
+                                           uint32_t *tab, uint32_t *rinfo) {
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < (1u << K); t += blockDim.x) rinfo[t] = A.rowinfo[c.grow(t, K) + chunk * A.n];
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < (20u << K); t += blockDim.x) {
+        const uint32_t j = t / 20, word = t - j * 20;
+        const uint32_t f = rinfo[j] & 0xFFFFu;
+        tab[t] = A.lut[(reveal ? 65535u - f : f) * 20u + word];
+    }
+    __syncthreads();
+}
+
+template <int K, int LR, bool PB, bool SCALE>
+__device__ __forceinline__ void load_rows(const PassArgs &A, const Ctx &c, uint32_t chunk, const uint32_t *tab,
+                                          const uint32_t *rinfo, uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
     using P = Pass<K, LR>;
     static_for<0, P::R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        const uint32_t r = c.grow(P::template lrow<PB>(c.w, i), K) + chunk * A.n;
+        const uint32_t j = P::template lrow<PB>(c.w, i);
+        uint32_t r = c.grow(j, K) + chunk * A.n;
+        r = __builtin_amdgcn_readfirstlane(r);
+        asm volatile("" : "+s"(r));  // keep the row's address math here, not hoisted
         const uint8_t *p = nullptr;
         if (A.work_in) {
             p = A.work_in + uint64_t(r) * A.work_stride;
         } else {
-            for (uint32_t k = 0; k < A.nsrc; ++k)
-                if (r >= A.src[k].row_begin && r < A.src[k].row_end)
-                    p = A.src[k].base + uint64_t(r - A.src[k].row_begin) * A.src[k].stride;
+            if (r >= A.src[0].row_begin && r < A.src[0].row_end)
+                p = A.src[0].base + uint64_t(r - A.src[0].row_begin) * A.src[0].stride;
+            if (A.nsrc > 1 && r >= A.src[1].row_begin && r < A.src[1].row_end)
+                p = A.src[1].base + uint64_t(r - A.src[1].row_begin) * A.src[1].stride;
         }
-        uint32_t ri = 0;
-        if (A.load_scale) {
-            ri = A.rowinfo[r];
-            if (ri & 0x10000u) p = nullptr;
-        }
+        if (SCALE && (rinfo[j] & 0x10000u)) p = nullptr;
         uint32_t l = 0, h = 0;
         if (p && c.pk_ok) {
             l = *reinterpret_cast<const uint32_t *>(p + c.pk_off);
             h = *reinterpret_cast<const uint32_t *>(p + c.pk_off + 32);
         }
-        if (A.load_scale && p) gf_mul4(l, h, A.lut + (ri & 0xFFFFu) * 20u);
         lo[i] = l;
         hi[i] = h;
     });
+    if constexpr (SCALE) {
+        uint32_t dep = 0;
+        static_for<0, P::R>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            uint32_t off = P::template lrow<PB>(c.w, i) * 20u;
+            asm volatile("" : "+s"(off), "+v"(lo[i]), "+v"(hi[i]) : "v"(dep));  // one row at a time
+            gf_mul4(lo[i], hi[i], tab + off);
+            dep = lo[i];
+        });
+    }
 }
 
-template <int K, int LR, bool PB>
-__device__ __forceinline__ void store_rows(const PassArgs &A, const Ctx &c, uint32_t chunk, uint32_t (&lo)[1 << LR],
-                                           uint32_t (&hi)[1 << LR]) {
+template <int K, int LR, bool PB, bool REVEAL>
+__device__ __forceinline__ void store_rows(const PassArgs &A, const Ctx &c, uint32_t chunk, const uint32_t *tab,
+                                           const uint32_t *rinfo, uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
     using P = Pass<K, LR>;
     static_for<0, P::R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        const uint32_t r = c.grow(P::template lrow<PB>(c.w, i), K) + chunk * A.n;
+        const uint32_t j = P::template lrow<PB>(c.w, i);
+        uint32_t r = c.grow(j, K) + chunk * A.n;
+        r = __builtin_amdgcn_readfirstlane(r);
+        asm volatile("" : "+s"(r));  // keep the row's address math here, not hoisted
         uint8_t *p = nullptr;
         uint32_t l = lo[i], h = hi[i];
         if (A.work_out) {
             p = A.work_out + uint64_t(r) * A.work_stride;
         } else if (r >= A.dst.row_begin && r < A.dst.row_end) {
             p = const_cast<uint8_t *>(A.dst.base) + uint64_t(r - A.dst.row_begin) * A.dst.stride;
-            if (A.reveal) {
-                const uint32_t ri = A.rowinfo[r];
-                if (ri & 0x10000u) gf_mul4(l, h, A.lut + (65535u - (ri & 0xFFFFu)) * 20u);
+            if constexpr (REVEAL) {
+                if (rinfo[j] & 0x10000u) gf_mul4(l, h, tab + j * 20u);
                 else p = nullptr;
             }
         }
@@ -164,76 +230,91 @@ __device__ __forceinline__ void store_rows(const PassArgs &A, const Ctx &c, uint
 
 // One butterfly layer on local bit B (global bit a + B), rows held in phase PB.
 template <int K, int LR, bool PB, int B, bool IFFT>
-__device__ __forceinline__ void layer(const PassArgs &A, const Ctx &c, uint32_t delta, uint32_t (&lo)[1 << LR],
+__device__ __forceinline__ void layer(const Ctx &c, const uint32_t *tab, uint32_t (&lo)[1 << LR],
                                       uint32_t (&hi)[1 << LR]) {
     using P = Pass<K, LR>;
     constexpr int RB = PB && P::W > 1 ? B - (K - LR) : B;  // register bit
     static_assert(RB >= 0 && RB < LR, "bit not resident in this phase");
-    const uint32_t gbit = c.a + B;
-    static_for<0, P::R>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        if constexpr ((i & (1 << RB)) == 0) {
+    // Butterfly groups of this layer held by the lane: register index bits
+    // above RB.  One 20-word table per group, read from LDS once and used for
+    // the group's 2^RB butterflies.  The table's address is tied (empty asm)
+    // to the previous group's result, so at most one table is in flight:
+    // otherwise the compiler hoists every table of the layer and spills.
+    uint32_t dep = 0;
+    static_for<0, (P::R >> (RB + 1))>([&](auto gc) {
+        constexpr int i0 = decltype(gc)::value << (RB + 1);
+        uint32_t off = tw_slot<K>(B, P::template lrow<PB>(c.w, i0)) * 20u;
+        asm volatile("" : "+s"(off) : "v"(dep));
+        const uint4 *t4 = reinterpret_cast<const uint4 *>(tab + off);
+        uint32_t t[20];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const uint4 v = t4[q];
+            t[4 * q] = v.x, t[4 * q + 1] = v.y, t[4 * q + 2] = v.z, t[4 * q + 3] = v.w;
+        }
+        static_for<0, (1 << RB)>([&](auto lc) {
+            constexpr int i = i0 | decltype(lc)::value;
             constexpr int i2 = i | (1 << RB);
-            const uint32_t g = c.grow(P::template lrow<PB>(c.w, i), K);
-            const uint32_t r = g & ~((2u << gbit) - 1u);
-            const uint32_t idx = r + (1u << gbit) + delta - 1u;
-            const uint32_t *t = A.tw + idx * 20u;
+            // The butterflies are independent; left alone the compiler
+            // interleaves all of them (~18 live VGPRs each) and spills.  Tie
+            // each one's inputs to the previous one's output: one butterfly
+            // in flight per wave, the other waves of the SIMD fill the gaps.
+            asm volatile("" : "+v"(lo[i]), "+v"(hi[i]), "+v"(lo[i2]), "+v"(hi[i2]) : "v"(dep));
             if constexpr (IFFT) ifft_bfly(lo[i], hi[i], lo[i2], hi[i2], t);
             else fft_bfly(lo[i], hi[i], lo[i2], hi[i2], t);
-        }
+            dep = lo[i];
+        });
     });
 }
 
+// Move the rows from phase FROM_B to phase TO_B through LDS, one plane at a time.
 template <int K, int LR, bool FROM_B, bool TO_B>
-__device__ __forceinline__ void exchange(const Ctx &c, uint32_t *lds, uint32_t (&lo)[1 << LR],
+__device__ __forceinline__ void exchange(const Ctx &c, uint32_t *plane, uint32_t (&lo)[1 << LR],
                                          uint32_t (&hi)[1 << LR]) {
     using P = Pass<K, LR>;
     if constexpr (P::W == 1 || FROM_B == TO_B) return;
-    uint32_t *llo = lds, *lhi = lds + (kLanes << K);
-    __syncthreads();
-    static_for<0, P::R>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        const uint32_t j = P::template lrow<FROM_B>(c.w, i);
-        llo[j * kLanes + c.lane] = lo[i];
-        lhi[j * kLanes + c.lane] = hi[i];
-    });
-    __syncthreads();
-    static_for<0, P::R>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        const uint32_t j = P::template lrow<TO_B>(c.w, i);
-        lo[i] = llo[j * kLanes + c.lane];
-        hi[i] = lhi[j * kLanes + c.lane];
-    });
+    auto one = [&](uint32_t(&v)[1 << LR]) {
+        __syncthreads();
+        static_for<0, P::R>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            plane[P::template lrow<FROM_B>(c.w, i) * kLanes + c.lane] = v[i];
+        });
+        __syncthreads();
+        static_for<0, P::R>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            v[i] = plane[P::template lrow<TO_B>(c.w, i) * kLanes + c.lane];
+        });
+    };
+    one(lo);
+    one(hi);
 }
 
-// Formal derivative restricted to the set's local bits:
+// Formal derivative restricted to the set's local bits, plane by plane:
 //   x[q] <- (mode 2 ? x[q] : 0) ^ XOR_{b < K, q_b = 0} x[q | 2^b]
 template <int K, int LR, bool PB>
-__device__ __forceinline__ void formal_derivative(const Ctx &c, uint32_t mode, uint32_t *lds,
+__device__ __forceinline__ void formal_derivative(const Ctx &c, uint32_t mode, uint32_t *plane,
                                                   uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
     using P = Pass<K, LR>;
-    uint32_t *llo = lds, *lhi = lds + (kLanes << K);
-    __syncthreads();
-    static_for<0, P::R>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        const uint32_t j = P::template lrow<PB>(c.w, i);
-        llo[j * kLanes + c.lane] = lo[i];
-        lhi[j * kLanes + c.lane] = hi[i];
-    });
-    __syncthreads();
-    static_for<0, P::R>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        const uint32_t j = P::template lrow<PB>(c.w, i);
-        uint32_t l = mode == 2 ? lo[i] : 0u, h = mode == 2 ? hi[i] : 0u;
+    auto one = [&](uint32_t(&v)[1 << LR]) {
+        __syncthreads();
+        static_for<0, P::R>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            plane[P::template lrow<PB>(c.w, i) * kLanes + c.lane] = v[i];
+        });
+        __syncthreads();
+        static_for<0, P::R>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            const uint32_t j = P::template lrow<PB>(c.w, i);
+            uint32_t acc = mode == 2 ? v[i] : 0u;
 #pragma unroll
-        for (int b = 0; b < K; ++b)
-            if (!(j & (1u << b))) {
-                l ^= llo[(j | (1u << b)) * kLanes + c.lane];
-                h ^= lhi[(j | (1u << b)) * kLanes + c.lane];
-            }
-        lo[i] = l;
-        hi[i] = h;
-    });
+            for (int b = 0; b < K; ++b)
+                if (!(j & (1u << b))) acc ^= plane[(j | (1u << b)) * kLanes + c.lane];
+            v[i] = acc;
+            asm volatile("" ::: "memory");
+        });
+    };
+    one(lo);
+    one(hi);
 }
 
 template <int K, int LR, bool PB>
@@ -242,7 +323,9 @@ __device__ __forceinline__ void xor_rows_in(const PassArgs &A, const Ctx &c, uin
     using P = Pass<K, LR>;
     static_for<0, P::R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        const uint32_t r = c.grow(P::template lrow<PB>(c.w, i), K);
+        uint32_t r = c.grow(P::template lrow<PB>(c.w, i), K);
+        r = __builtin_amdgcn_readfirstlane(r);
+        asm volatile("" : "+s"(r));
         const uint8_t *p = A.xor_in + uint64_t(r) * A.work_stride;
         if (c.pk_ok) {
             lo[i] ^= *reinterpret_cast<const uint32_t *>(p + c.pk_off);
@@ -251,13 +334,45 @@ __device__ __forceinline__ void xor_rows_in(const PassArgs &A, const Ctx &c, uin
     });
 }
 
+template <int K, int LR, bool IFFT>
+__device__ __forceinline__ void transform(const Ctx &c, uint32_t *plane, const uint32_t *tab,
+                                          uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
+    using P = Pass<K, LR>;
+    constexpr bool HAS_B = P::W > 1;
+    if constexpr (IFFT) {  // bits ascending: A-phase [0, LR), B-phase [LR, K)
+        static_for<0, (LR < K ? LR : K)>([&](auto bc) { layer<K, LR, false, decltype(bc)::value, true>(c, tab, lo, hi); });
+        if constexpr (HAS_B) {
+            exchange<K, LR, false, true>(c, plane, lo, hi);
+            static_for<LR, K>([&](auto bc) { layer<K, LR, true, decltype(bc)::value, true>(c, tab, lo, hi); });
+        }
+    } else {  // bits descending: B-phase [LR, K), A-phase [0, LR)
+        if constexpr (HAS_B) {
+            static_for<0, K - LR>([&](auto bc) { layer<K, LR, true, K - 1 - decltype(bc)::value, false>(c, tab, lo, hi); });
+            exchange<K, LR, true, false>(c, plane, lo, hi);
+        }
+        static_for<0, (LR < K ? LR : K)>([&](auto bc) {
+            constexpr int b = (LR < K ? LR : K) - 1 - decltype(bc)::value;
+            layer<K, LR, false, b, false>(c, tab, lo, hi);
+        });
+    }
+}
+
 template <int K, int LR, int FLAGS>
-__global__ void __launch_bounds__(kLanes << (K - LR)) k_pass(const PassArgs A) {
+__global__ void __launch_bounds__(kLanes << (K - LR), 2) k_pass(const PassArgs A) {
     using P = Pass<K, LR>;
     constexpr bool DO_IFFT = FLAGS & kIfft;
     constexpr bool DO_FFT = FLAGS & kFft;
+    constexpr bool MULTI_IN = FLAGS & kMultiIn;    // XOR-fold IFFTs of A.in_chunks chunks
+    constexpr bool MULTI_OUT = FLAGS & kMultiOut;  // FFT the same rows for A.out_chunks chunks
+    constexpr bool SCALE = FLAGS & kScale;         // decode: scale received rows, zero erased ones
+    constexpr bool FD = FLAGS & kFd;               // decode: formal derivative over local bits
+    constexpr bool XOR_IN = FLAGS & kXorIn;        // decode: x ^= rows of A.xor_in
+    constexpr bool REVEAL = FLAGS & kReveal;       // decode: store erased originals, unscaled
     constexpr bool HAS_B = P::W > 1;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t *plane = lds;
+    uint32_t *tab = lds + Lds<K>::kPlane;
+    uint32_t *rinfo = tab + Lds<K>::kTab;
 
     Ctx c;
     c.lane = threadIdx.x & (kLanes - 1);
@@ -275,17 +390,19 @@ __global__ void __launch_bounds__(kLanes << (K - LR)) k_pass(const PassArgs A) {
     uint32_t lo[P::R], hi[P::R];
 
     // ---- load (+ IFFT per input chunk, XOR-accumulated) ------------------
-    if constexpr (DO_IFFT) {
+    if constexpr (DO_IFFT && !MULTI_IN) {
+        if constexpr (SCALE) stage_rows<K>(A, c, gchunk, false, tab, rinfo);
+        load_rows<K, LR, false, SCALE>(A, c, gchunk, tab, rinfo, lo, hi);
+        if constexpr (K > 0) stage_twiddles<K>(A, c, A.ifft_delta + gchunk * A.ifft_delta_step, tab);
+        transform<K, LR, true>(c, plane, tab, lo, hi);
+    } else if constexpr (DO_IFFT) {
         uint32_t tl[P::R], th[P::R];
         for (uint32_t ci = 0; ci < A.in_chunks; ++ci) {
             const uint32_t chunk = gchunk + ci;
-            load_rows<K, LR, false>(A, c, chunk, tl, th);
-            const uint32_t delta = A.ifft_delta + chunk * A.ifft_delta_step;
-            static_for<0, LR < K ? LR : K>([&](auto bc) { layer<K, LR, false, decltype(bc)::value, true>(A, c, delta, tl, th); });
-            if constexpr (HAS_B) {
-                exchange<K, LR, false, true>(c, lds, tl, th);
-                static_for<LR, K>([&](auto bc) { layer<K, LR, true, decltype(bc)::value, true>(A, c, delta, tl, th); });
-            }
+            if constexpr (SCALE) stage_rows<K>(A, c, chunk, false, tab, rinfo);
+            load_rows<K, LR, false, SCALE>(A, c, chunk, tab, rinfo, tl, th);
+            if constexpr (K > 0) stage_twiddles<K>(A, c, A.ifft_delta + chunk * A.ifft_delta_step, tab);
+            transform<K, LR, true>(c, plane, tab, tl, th);
             if (ci == 0) {
                 static_for<0, P::R>([&](auto ic) { lo[ic] = tl[ic]; hi[ic] = th[ic]; });
             } else {
@@ -293,54 +410,40 @@ __global__ void __launch_bounds__(kLanes << (K - LR)) k_pass(const PassArgs A) {
             }
         }
     } else {
-        load_rows<K, LR, HAS_B>(A, c, gchunk, lo, hi);
+        if constexpr (SCALE) stage_rows<K>(A, c, gchunk, false, tab, rinfo);
+        load_rows<K, LR, HAS_B, SCALE>(A, c, gchunk, tab, rinfo, lo, hi);
     }
     // rows are now in phase B (if the pass has one)
 
-    if (A.fd_mode) formal_derivative<K, LR, HAS_B>(c, A.fd_mode, lds, lo, hi);
-    if (A.xor_in) xor_rows_in<K, LR, HAS_B>(A, c, lo, hi);
+    if constexpr (FD) formal_derivative<K, LR, HAS_B>(c, A.fd_mode, plane, lo, hi);
+    if constexpr (XOR_IN) xor_rows_in<K, LR, HAS_B>(A, c, lo, hi);
 
     // ---- FFT per output chunk + store ------------------------------------
-    if constexpr (DO_FFT) {
+    if constexpr (DO_FFT && !MULTI_OUT) {
+        if constexpr (K > 0) stage_twiddles<K>(A, c, A.fft_delta + gchunk * A.fft_delta_step, tab);
+        transform<K, LR, false>(c, plane, tab, lo, hi);
+        if constexpr (REVEAL) stage_rows<K>(A, c, gchunk, true, tab, rinfo);
+        store_rows<K, LR, false, REVEAL>(A, c, gchunk, tab, rinfo, lo, hi);
+    } else if constexpr (DO_FFT) {
         for (uint32_t co = 0; co < A.out_chunks; ++co) {
             const uint32_t chunk = gchunk + co;
-            const uint32_t delta = A.fft_delta + chunk * A.fft_delta_step;
             uint32_t yl[P::R], yh[P::R];
             static_for<0, P::R>([&](auto ic) { yl[ic] = lo[ic]; yh[ic] = hi[ic]; });
-            if constexpr (HAS_B) {
-                static_for<0, K - LR>([&](auto bc) {
-                    constexpr int b = K - 1 - decltype(bc)::value;
-                    layer<K, LR, true, b, false>(A, c, delta, yl, yh);
-                });
-                exchange<K, LR, true, false>(c, lds, yl, yh);
-                static_for<0, LR>([&](auto bc) {
-                    constexpr int b = LR - 1 - decltype(bc)::value;
-                    layer<K, LR, false, b, false>(A, c, delta, yl, yh);
-                });
-            } else {
-                static_for<0, K>([&](auto bc) {
-                    constexpr int b = K - 1 - decltype(bc)::value;
-                    layer<K, LR, false, b, false>(A, c, delta, yl, yh);
-                });
-            }
-            store_rows<K, LR, false>(A, c, chunk, yl, yh);
+            if constexpr (K > 0) stage_twiddles<K>(A, c, A.fft_delta + chunk * A.fft_delta_step, tab);
+            transform<K, LR, false>(c, plane, tab, yl, yh);
+            if constexpr (REVEAL) stage_rows<K>(A, c, chunk, true, tab, rinfo);
+            store_rows<K, LR, false, REVEAL>(A, c, chunk, tab, rinfo, yl, yh);
         }
     } else {
-        store_rows<K, LR, HAS_B>(A, c, gchunk, lo, hi);
+        if constexpr (REVEAL) stage_rows<K>(A, c, gchunk, true, tab, rinfo);
+        store_rows<K, LR, HAS_B, REVEAL>(A, c, gchunk, tab, rinfo, lo, hi);
     }
 }
-
-// Note on phases: with HAS_B the IFFT leaves rows in phase B and the FFT ends
-// in phase A; without FFT the store happens in phase B.  The layer bits in
-// phase B are [K-LR, K): the IFFT's B-layers run over [LR, K) which is inside
-// it because K <= 2*LR.  The FFT's B-layers run over [LR, K) as well
-// (descending), its A-layers over [0, LR).
 
 template <int K, int LR, int F>
 hipError_t launch_f(const PassArgs &A, hipStream_t s) {
     using P = Pass<K, LR>;
-    // LDS: one [2^K rows][64 lanes] tile of low words + one of high words
-    const size_t lds = size_t(8) * kLanes << K;
+    const size_t lds = Lds<K>::bytes();
     static bool attr_set = false;  // benign race: idempotent attribute call
     if (!attr_set && lds > 65536) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pass<K, LR, F>),
@@ -355,11 +458,29 @@ hipError_t launch_f(const PassArgs &A, hipStream_t s) {
 
 template <int K, int LR>
 hipError_t launch_k(int flags, const PassArgs &A, hipStream_t s) {
+    if (A.in_chunks > 1) flags |= kMultiIn;
+    if (A.out_chunks > 1) flags |= kMultiOut;
+    if (A.load_scale) flags |= kScale;
+    if (A.fd_mode) flags |= kFd;
+    if (A.xor_in) flags |= kXorIn;
+    if (A.reveal) flags |= kReveal;
+    constexpr int I = kIfft, F = kFft;
     switch (flags) {
-        case kIfft: return launch_f<K, LR, kIfft>(A, s);
-        case kFft: return launch_f<K, LR, kFft>(A, s);
-        case kIfft | kFft: return launch_f<K, LR, kIfft | kFft>(A, s);
-        default: return launch_f<K, LR, 0>(A, s);
+        // encode / engine
+        case I: return launch_f<K, LR, I>(A, s);
+        case F: return launch_f<K, LR, F>(A, s);
+        case I | F: return launch_f<K, LR, I | F>(A, s);
+        case I | kMultiIn: return launch_f<K, LR, I | kMultiIn>(A, s);
+        case I | F | kMultiIn: return launch_f<K, LR, I | F | kMultiIn>(A, s);
+        case I | F | kMultiOut: return launch_f<K, LR, I | F | kMultiOut>(A, s);
+        case F | kMultiOut: return launch_f<K, LR, F | kMultiOut>(A, s);
+        // decode: single pass, IFFT passes, fused top, FFT passes (middle / last)
+        case I | F | kScale | kFd | kReveal: return launch_f<K, LR, I | F | kScale | kFd | kReveal>(A, s);
+        case I | kScale: return launch_f<K, LR, I | kScale>(A, s);
+        case I | F | kFd: return launch_f<K, LR, I | F | kFd>(A, s);
+        case F | kFd | kXorIn: return launch_f<K, LR, F | kFd | kXorIn>(A, s);
+        case F | kFd | kXorIn | kReveal: return launch_f<K, LR, F | kFd | kXorIn | kReveal>(A, s);
+        default: return hipErrorInvalidValue;
     }
 }
 
@@ -444,8 +565,6 @@ hipError_t launch_pass(int K, int flags, const PassArgs &A, hipStream_t s) {
         case 4: return launch_k<4, 2>(flags, A, s);
         case 5: return launch_k<5, 3>(flags, A, s);
         case 6: return launch_k<6, 3>(flags, A, s);
-        case 7: return launch_k<7, 4>(flags, A, s);
-        case 8: return launch_k<8, 4>(flags, A, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -98,6 +98,25 @@ for _t in ("exp", "log", "skew", "log_walsh"):
     _sig(f"rs_table_{_t}", ctypes.POINTER(ctypes.c_uint16))
 for _t in ("perm_by_log", "perm_by_skew"):
     _sig(f"rs_table_{_t}", ctypes.POINTER(ctypes.c_uint32))
+_sig("rs_profile_enable", _int, _vp, _int)
+_sig("rs_profile_collect", _int, _vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(_u64),
+     ctypes.POINTER(ctypes.c_char_p), _int)
+
+
+def profile_enable(enable: bool = True, ctx=None) -> None:
+    """Bracket every kernel launch of `ctx` with HIP events (bench instrumentation)."""
+    ctx = ctx or default_context()
+    _lib.rs_profile_enable(ctx.handle, 1 if enable else 0)
+
+
+def profile_collect(ctx=None, max_records: int = 1 << 16):
+    """[(kernel_name, ms, algorithmic_bytes)] of the launches since the last collect."""
+    ctx = ctx or default_context()
+    ms = (ctypes.c_float * max_records)()
+    by = (_u64 * max_records)()
+    nm = (ctypes.c_char_p * max_records)()
+    n = _lib.rs_profile_collect(ctx.handle, ms, by, nm, max_records)
+    return [(nm[i].decode(), float(ms[i]), int(by[i])) for i in range(max(n, 0))]
 
 GF_BITS = 16
 GF_ORDER = 65536
@@ -574,12 +593,21 @@ def encode_device(original_count: int, recovery_count: int, shard_bytes: int, d_
                                  _ptr(d_recovery), _stream(stream), ctypes.byref(err)), err)
 
 
+def present_mask(flags) -> bytes:
+    """0/1 byte mask; bytes pass through unchanged (pre-build it once in hot loops)."""
+    if isinstance(flags, (bytes, bytearray)):
+        return bytes(flags)
+    if hasattr(flags, "astype"):
+        return (flags != 0).astype("uint8").tobytes()
+    return bytes(bytearray(1 if x else 0 for x in flags))
+
+
 def decode_device(original_count: int, recovery_count: int, shard_bytes: int, d_original, original_present,
                   d_recovery, recovery_present, d_restored, stream=None, rate_: int = RATE_DEFAULT,
                   ctx: Optional[Context] = None) -> None:
     ctx = ctx or default_context()
-    op = bytes(bytearray(1 if x else 0 for x in original_present))
-    rp = bytes(bytearray(1 if x else 0 for x in recovery_present))
+    op = present_mask(original_present)
+    rp = present_mask(recovery_present)
     err = _RsError()
     _raise(_lib.rs_decode_device(ctx.handle, rate_, original_count, recovery_count, shard_bytes, _ptr(d_original), op,
                                  _ptr(d_recovery), rp, _ptr(d_restored), _stream(stream), ctypes.byref(err)), err)
