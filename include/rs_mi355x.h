@@ -186,6 +186,16 @@ rs_status rs_engine_formal_derivative(rs_context *ctx, void *d_rows, uint64_t sh
 rs_status rs_profile_enable(rs_context *ctx, int enable);
 int rs_profile_collect(rs_context *ctx, float *ms, uint64_t *bytes, const char **names, int max);
 
+/* ---- chain kernel control (engine tuning, not a reference item) ----
+ * Small 2-level transforms run their three passes in one launch whose
+ * workgroups meet at in-kernel barriers (DESIGN.md "Chain kernel").
+ * rs_chain_enable(ctx, 0) forces one launch per pass (also: environment
+ * RS_MI355X_NO_CHAIN=1 at context creation).  rs_check_device synchronizes
+ * the device and returns RS_ERR_DEVICE if an in-kernel barrier wait timed out
+ * (results of that launch are invalid) since the last check, else RS_OK. */
+rs_status rs_chain_enable(rs_context *ctx, int enable);
+rs_status rs_check_device(rs_context *ctx);
+
 /* ---- GF(2^16) tables (src/engine/tables.rs), host copies ---- */
 const uint16_t *rs_table_exp(void);       /* 65536 */
 const uint16_t *rs_table_log(void);       /* 65536 */

@@ -69,6 +69,22 @@ enum PassFlags {
 // Launch one pass on `stream`.  K = log2(rows per set).
 hipError_t launch_pass(int K, int flags, const PassArgs &args, hipStream_t stream);
 
+// Three passes of a 2-level transform in one launch (DESIGN.md "Chain
+// kernel"): phase 0 = level 0 (K0 bits), phase 1 = fused top level (K1 bits),
+// phase 2 = level 0 again.  Every PassArgs has the same `slices` (packs per
+// slice 2^spl); the grid is slices x members workgroups and member q runs
+// blocks q, q + members, ... of each phase's items (set + chunk * nsets).
+enum ChainMode { kChainEncodeHigh = 0, kChainEncodeLow = 1, kChainDecode = 2 };
+struct ChainArgs {
+    PassArgs ph[3];
+    uint32_t items[3] = {0, 0, 0};
+    uint32_t members = 0;
+    uint32_t *sync = nullptr;   // 32 words per slice, zero between launches
+    uint32_t *fault = nullptr;  // set if a barrier wait gave up
+};
+// hipErrorNotSupported: no chain kernel for this (K0, K1, spl).
+hipError_t launch_chain(int mode, int K0, int K1, int spl, const ChainArgs &C, hipStream_t stream);
+
 // eval_poly for a decode: erasure vector -> per-row log factors.
 //   state[r] (r < 2^u): bit0 = erasure-vector entry, bit1 = row received.
 //   low_rate: the erasure vector is also 1 on [2^u, 65536) (rate_low.rs:196).

@@ -11,8 +11,8 @@
 // 32-bit word of low bytes + one of high bytes (the reference's block layout),
 // and v_perm_b32 performs 4 byte lookups into an 8-entry table at once
 // (12 v_perm + 10 field extracts + 6 v_bitop3 XOR3 per 4 elements).
-// The twiddle of a butterfly group is wave-uniform: lanes run along the
-// columns of one row pair, so each table arrives through scalar loads.
+// Lanes run along the columns (packs) of the shard matrix; the twiddle tables
+// of a pass are staged in LDS once per workgroup.
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -22,8 +22,6 @@
 namespace rs {
 namespace {
 
-constexpr int kLanes = 64;
-
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for(F &&f) {
     if constexpr (I < N) {
@@ -31,6 +29,14 @@ __device__ __forceinline__ void static_for(F &&f) {
         static_for<I + 1, N>(f);
     }
 }
+
+#ifdef RS_CHAIN_STAMPS  // tools/chain_probe.hip: per-workgroup timestamps
+__device__ uint64_t g_chain_stamps[4096][32];
+#define RS_STAMP(i) \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_chain_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime()
+#else
+#define RS_STAMP(i)
+#endif
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -79,46 +85,107 @@ __device__ __forceinline__ void fft_bfly(uint32_t &al, uint32_t &ah, uint32_t &b
 }
 
 // -------------------------------------------------------------------------
-// Pass kernel.  K: log2 rows per set; LR: log2 rows held per lane.
-// Waves W = 2^(K-LR).  Phase A: a wave holds local rows (w << LR) | i
-// (bits [0,LR) in registers).  Phase B: rows (i << (K-LR)) | w (bits
-// [K-LR, K) in registers).  K <= 2*LR, so IFFT = A-layers then B-layers and
-// FFT = B-layers then A-layers, with one LDS exchange each.
-template <int K, int LR>
+// Pass kernel.
+//   K   : log2 rows per set (the butterfly layers this pass runs)
+//   LR  : log2 rows a lane holds in registers
+//   SPL : log2 packs per workgroup column slice
+// A workgroup is G = 2^(K-LR) row groups x SP packs: thread t works on pack
+// t % SP of row group g = t / SP.  The K local row bits are covered by
+// register PHASES: in phase p a lane's registers run over local row bits
+// [s_p, s_p + LR), s_p = min(p*LR, K-LR), the remaining bits come from g.
+// Layer b runs in phase min(b / LR, NPH - 1); a phase change is an exchange
+// of the rows through LDS.  Small slices (SPL < 6) spread a small shard matrix
+// over more workgroups; then g differs inside a wave and row addresses and
+// twiddle tables are per lane instead of wave-uniform.
+template <int K, int LR, int SPL>
 struct Pass {
     static constexpr int R = 1 << LR;
-    static constexpr int W = 1 << (K - LR);
-    static constexpr int kThreads = kLanes * W;
-    static_assert(K <= 2 * LR, "two register phases must cover all local bits");
+    static constexpr int SP = 1 << SPL;
+    static constexpr int G = 1 << (K - LR);
+    static constexpr int kThreads = SP * G;
+    static constexpr int NPH = K == 0 ? 1 : (K + LR - 1) / LR;
+    static constexpr bool kUniform = SPL >= 6;
+    // Left alone, the compiler interleaves every butterfly of a layer and
+    // hoists all their tables: with 8 rows per lane that costs occupancy or
+    // spills, so wide shapes run one table / butterfly at a time per wave.
+    static constexpr bool kChain = R >= 8;
+    static_assert(K == 0 || (LR >= 1 && LR <= K), "register bits must fit the set");
+    static_assert(kThreads >= 64, "at least one full wave");
 
-    template <bool PB>
-    static __device__ __forceinline__ uint32_t lrow(uint32_t w, int i) {
-        // '+' (not '|': the bits are disjoint) lets the compiler fold the
-        // register index into LDS / global immediate offsets
-        if constexpr (W == 1) return i;
-        if constexpr (PB) return (uint32_t(i) << (K - LR)) + w;
-        return (w << LR) + uint32_t(i);
+    static constexpr int start(int p) { return p * LR < K - LR ? p * LR : K - LR; }
+    static constexpr int phase_of(int b) { return LR == 0 || b / (LR ? LR : 1) >= NPH - 1 ? NPH - 1 : b / (LR ? LR : 1); }
+
+    // local row held in register i in phase PH ('+': disjoint bits, lets the
+    // register index fold into immediate offsets)
+    template <int PH>
+    static __device__ __forceinline__ uint32_t lrow(uint32_t g, int i) {
+        if constexpr (G == 1) {
+            return uint32_t(i);
+        } else {
+            constexpr int s = start(PH);
+            const uint32_t lo = g & ((1u << s) - 1u), hi = g >> s;
+            return lo + (uint32_t(i) << s) + (hi << (s + LR));
+        }
     }
 };
 
 struct Ctx {
-    uint32_t lane, w, s_lo, s_hi, a, pk_off;
+    uint32_t g, p, s_lo, s_hi, a, pk_off;
     bool pk_ok;
     __device__ __forceinline__ uint32_t grow(uint32_t j, int K) const { return s_lo + (j << a) + (s_hi << (a + K)); }
 };
 
+// Keep a row index's address math at its use (not hoisted, which costs
+// registers); wave-uniform indices stay scalar.
+template <bool UNIFORM>
+__device__ __forceinline__ uint32_t pin(uint32_t r) {
+    if constexpr (UNIFORM) {
+        r = __builtin_amdgcn_readfirstlane(r);
+        asm volatile("" : "+s"(r));
+    } else {
+        asm volatile("" : "+v"(r));
+    }
+    return r;
+}
+
+// Row words of the work buffers.  COH: write-through / coherent accesses
+// (agent-scope relaxed atomics: global_load/store sc1) for rows handed
+// between workgroups inside one launch (k_chain, DESIGN.md "Chain kernel").
+template <bool COH>
+__device__ __forceinline__ uint32_t ld32(const uint8_t *p) {
+    if constexpr (COH)
+        return __hip_atomic_load(reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(p)), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    else
+        return *reinterpret_cast<const uint32_t *>(p);
+}
+template <bool COH>
+__device__ __forceinline__ void st32(uint8_t *p, uint32_t v) {
+    if constexpr (COH)
+        __hip_atomic_store(reinterpret_cast<uint32_t *>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *reinterpret_cast<uint32_t *>(p) = v;
+}
+
 // LDS layout (dynamic, 16-byte aligned), in 32-bit words:
-//   plane : 64 lanes x 2^K rows, one data plane (low or high words) at a time
-//   tab   : 2^K tables x 20 words -- the twiddle tables of the transform in
-//           flight (slot = 2^K - 2^(K-b) + group, b = local layer), or the
-//           per-row scale tables of a decode load / reveal
-//   rinfo : 2^K words -- decode row info of the set's rows
-template <int K>
+//   planes : 2 x (2^K rows x SP packs): low and high words of the exchange
+//   tabI   : 2^K - 1 twiddle tables (20 words) of the IFFT in flight
+//   tabF   : same for the FFT          (slot = 2^K - 2^(K-b) + group, b = local layer)
+//   tabS   : per-row scale tables of a decode load   (log factor f)
+//   tabV   : per-row tables of a decode reveal       (log factor 65535 - f)
+//   rinfo  : decode row info of the set's rows
+template <int K, int SPL, int FLAGS>
 struct Lds {
-    static constexpr uint32_t kPlane = uint32_t(kLanes) << K;
+    static constexpr uint32_t kPlane = uint32_t(1u << SPL) << K;
     static constexpr uint32_t kTab = 20u << K;
-    static constexpr uint32_t kRows = 1u << K;
-    static constexpr size_t bytes() { return size_t(kPlane + kTab + kRows) * 4; }
+    static constexpr bool I = FLAGS & kIfft, F = FLAGS & kFft, S = FLAGS & kScale, V = FLAGS & kReveal;
+    static constexpr uint32_t oI = 2 * kPlane;
+    static constexpr uint32_t oF = oI + (I ? kTab : 0);
+    static constexpr uint32_t oS = oF + (F ? kTab : 0);
+    static constexpr uint32_t oV = oS + (S ? kTab : 0);
+    static constexpr uint32_t oR = oV + (V ? kTab : 0);
+    static constexpr uint32_t words = oR + ((S || V) ? (1u << K) : 0);
+    static constexpr size_t bytes() { return size_t(words) * 4; }
 };
 
 // slot of the twiddle table of local layer b for local row j (bit b of j clear)
@@ -127,49 +194,92 @@ __device__ __forceinline__ uint32_t tw_slot(int b, uint32_t j) {
     return (1u << K) - (1u << (K - b)) + (j >> (b + 1));
 }
 
-// Stage the 2^K - 1 twiddle tables of this set for one transform into LDS.
+// Word t of the set's twiddle tables of a transform with skew offset delta.
 template <int K>
-__device__ __forceinline__ void stage_twiddles(const PassArgs &A, const Ctx &c, uint32_t delta, uint32_t *tab) {
-    constexpr uint32_t slots = (1u << K) - 1;
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < slots * 20; t += blockDim.x) {
-        const uint32_t slot = t / 20, word = t - slot * 20;
-        const uint32_t y = (1u << K) - slot;                  // in [2, 2^K]
-        const int b = K - (32 - __builtin_clz(y - 1));        // K - ceil(log2 y)
-        const uint32_t g = slot - ((1u << K) - (1u << (K - b)));
-        const uint32_t row = c.grow(g << (b + 1), K);
-        const uint32_t gb = c.a + b;
-        const uint32_t idx = (row & ~((2u << gb) - 1u)) + (1u << gb) + delta - 1u;
-        tab[t] = A.tw[idx * 20u + word];
-    }
-    __syncthreads();
+__device__ __forceinline__ uint32_t twiddle_word(const PassArgs &A, const Ctx &c, uint32_t delta, uint32_t t) {
+    const uint32_t slot = t / 20, word = t - slot * 20;
+    const uint32_t y = (1u << K) - slot;            // in [2, 2^K]
+    const int b = K - (32 - __builtin_clz(y - 1));  // K - ceil(log2 y)
+    const uint32_t grp = slot - ((1u << K) - (1u << (K - b)));
+    const uint32_t row = c.grow(grp << (b + 1), K);
+    const uint32_t gb = c.a + b;
+    const uint32_t idx = (row & ~((2u << gb) - 1u)) + (1u << gb) + delta - 1u;
+    return A.tw[idx * 20u + word];
 }
 
-// Stage per-row decode info and scale tables (load: factor, reveal: 65535 - factor).
-template <int K>
-__device__ __forceinline__ void stage_rows(const PassArgs &A, const Ctx &c, uint32_t chunk, bool reveal,
-                                           uint32_t *tab, uint32_t *rinfo) {
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < (1u << K); t += blockDim.x) rinfo[t] = A.rowinfo[c.grow(t, K) + chunk * A.n];
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < (20u << K); t += blockDim.x) {
-        const uint32_t j = t / 20, word = t - j * 20;
-        const uint32_t f = rinfo[j] & 0xFFFFu;
-        tab[t] = A.lut[(reveal ? 65535u - f : f) * 20u + word];
+// Stage tables into LDS (null destinations are skipped).  No barrier.  NT =
+// workgroup size: each thread issues all its global loads before its LDS
+// stores, so staging costs one memory round trip (two for decode tables,
+// whose address depends on the row's log factor).
+template <int K, int NT>
+__device__ __forceinline__ void stage(const PassArgs &A, const Ctx &c, uint32_t chunk, uint32_t *tabI, uint32_t dI,
+                                      uint32_t *tabF, uint32_t dF, uint32_t *tabS, uint32_t *tabV,
+                                      uint32_t *rinfo) {
+    constexpr uint32_t kTw = ((1u << K) - 1) * 20, kRw = 20u << K;
+    constexpr int PT = kTw ? (kTw + NT - 1) / NT : 1, PR = (kRw + NT - 1) / NT;
+    const uint32_t tid = threadIdx.x;
+#ifdef RS_PROBE_SKIP_STAGE  // tools/pass_probe.hip: time a pass without table staging
+    return;
+#endif
+    uint32_t vi[PT], vf[PT];
+    if (tabI || tabF) {
+#pragma unroll
+        for (int k = 0; k < PT; ++k) {
+            const uint32_t t = tid + uint32_t(k) * NT;
+            if (t < kTw) {
+                if (tabI) vi[k] = twiddle_word<K>(A, c, dI, t);
+                if (tabF) vf[k] = twiddle_word<K>(A, c, dF, t);
+            }
+        }
     }
-    __syncthreads();
+    if (tabS || tabV) {
+        uint32_t f[PR], vs[PR], vv[PR];
+#pragma unroll
+        for (int k = 0; k < PR; ++k) {
+            const uint32_t t = tid + uint32_t(k) * NT;
+            if (t < kRw) f[k] = A.rowinfo[c.grow(t / 20, K) + chunk * A.n];
+        }
+        if (tid < (1u << K)) rinfo[tid] = A.rowinfo[c.grow(tid, K) + chunk * A.n];
+#pragma unroll
+        for (int k = 0; k < PR; ++k) {
+            const uint32_t t = tid + uint32_t(k) * NT;
+            if (t < kRw) {
+                const uint32_t word = t % 20, lf = f[k] & 0xFFFFu;
+                if (tabS) vs[k] = A.lut[lf * 20u + word];
+                if (tabV) vv[k] = A.lut[(65535u - lf) * 20u + word];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < PR; ++k) {
+            const uint32_t t = tid + uint32_t(k) * NT;
+            if (t < kRw) {
+                if (tabS) tabS[t] = vs[k];
+                if (tabV) tabV[t] = vv[k];
+            }
+        }
+    }
+    if (tabI || tabF) {
+#pragma unroll
+        for (int k = 0; k < PT; ++k) {
+            const uint32_t t = tid + uint32_t(k) * NT;
+            if (t < kTw) {
+                if (tabI) tabI[t] = vi[k];
+                if (tabF) tabF[t] = vf[k];
+            }
+        }
+    }
 }
 
-template <int K, int LR, bool PB, bool SCALE>
-__device__ __forceinline__ void load_rows(const PassArgs &A, const Ctx &c, uint32_t chunk, const uint32_t *tab,
-                                          const uint32_t *rinfo, uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
-    using P = Pass<K, LR>;
+// Load the lane's rows (phase PH) of `chunk`.  SCALE: rows erased in the
+// decode's erasure vector load as zero (checked in global rowinfo, so the
+// load need not wait for staging).
+template <int K, int LR, int SPL, int PH, bool SCALE, bool COH = false>
+__device__ __forceinline__ void load_rows(const PassArgs &A, const Ctx &c, uint32_t chunk, uint32_t (&lo)[1 << LR],
+                                          uint32_t (&hi)[1 << LR]) {
+    using P = Pass<K, LR, SPL>;
     static_for<0, P::R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        const uint32_t j = P::template lrow<PB>(c.w, i);
-        uint32_t r = c.grow(j, K) + chunk * A.n;
-        r = __builtin_amdgcn_readfirstlane(r);
-        asm volatile("" : "+s"(r));  // keep the row's address math here, not hoisted
+        const uint32_t r = pin<P::kUniform>(c.grow(P::template lrow<PH>(c.g, i), K) + chunk * A.n);
         const uint8_t *p = nullptr;
         if (A.work_in) {
             p = A.work_in + uint64_t(r) * A.work_stride;
@@ -179,37 +289,42 @@ __device__ __forceinline__ void load_rows(const PassArgs &A, const Ctx &c, uint3
             if (A.nsrc > 1 && r >= A.src[1].row_begin && r < A.src[1].row_end)
                 p = A.src[1].base + uint64_t(r - A.src[1].row_begin) * A.src[1].stride;
         }
-        if (SCALE && (rinfo[j] & 0x10000u)) p = nullptr;
+        if (SCALE && (A.rowinfo[r] & 0x10000u)) p = nullptr;
         uint32_t l = 0, h = 0;
         if (p && c.pk_ok) {
-            l = *reinterpret_cast<const uint32_t *>(p + c.pk_off);
-            h = *reinterpret_cast<const uint32_t *>(p + c.pk_off + 32);
+            l = ld32<COH>(p + c.pk_off);
+            h = ld32<COH>(p + c.pk_off + 32);
         }
         lo[i] = l;
         hi[i] = h;
     });
-    if constexpr (SCALE) {
-        uint32_t dep = 0;
-        static_for<0, P::R>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            uint32_t off = P::template lrow<PB>(c.w, i) * 20u;
-            asm volatile("" : "+s"(off), "+v"(lo[i]), "+v"(hi[i]) : "v"(dep));  // one row at a time
-            gf_mul4(lo[i], hi[i], tab + off);
-            dep = lo[i];
-        });
-    }
 }
 
-template <int K, int LR, bool PB, bool REVEAL>
-__device__ __forceinline__ void store_rows(const PassArgs &A, const Ctx &c, uint32_t chunk, const uint32_t *tab,
-                                           const uint32_t *rinfo, uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
-    using P = Pass<K, LR>;
+template <int K, int LR, int SPL, int PH>
+__device__ __forceinline__ void scale_rows(const Ctx &c, const uint32_t *tabS, uint32_t (&lo)[1 << LR],
+                                           uint32_t (&hi)[1 << LR]) {
+    using P = Pass<K, LR, SPL>;
+    uint32_t dep = 0;
     static_for<0, P::R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        const uint32_t j = P::template lrow<PB>(c.w, i);
-        uint32_t r = c.grow(j, K) + chunk * A.n;
-        r = __builtin_amdgcn_readfirstlane(r);
-        asm volatile("" : "+s"(r));  // keep the row's address math here, not hoisted
+        uint32_t off = P::template lrow<PH>(c.g, i) * 20u;
+        if constexpr (P::kChain) {
+            if constexpr (P::kUniform) asm volatile("" : "+s"(off), "+v"(lo[i]), "+v"(hi[i]) : "v"(dep));
+            else asm volatile("" : "+v"(off), "+v"(lo[i]), "+v"(hi[i]) : "v"(dep));
+        }
+        gf_mul4(lo[i], hi[i], tabS + off);
+        dep = lo[i];
+    });
+}
+
+template <int K, int LR, int SPL, int PH, bool REVEAL, bool COH = false>
+__device__ __forceinline__ void store_rows(const PassArgs &A, const Ctx &c, uint32_t chunk, const uint32_t *tabV,
+                                           const uint32_t *rinfo, uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
+    using P = Pass<K, LR, SPL>;
+    static_for<0, P::R>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const uint32_t j = P::template lrow<PH>(c.g, i);
+        const uint32_t r = pin<P::kUniform>(c.grow(j, K) + chunk * A.n);
         uint8_t *p = nullptr;
         uint32_t l = lo[i], h = hi[i];
         if (A.work_out) {
@@ -217,34 +332,34 @@ __device__ __forceinline__ void store_rows(const PassArgs &A, const Ctx &c, uint
         } else if (r >= A.dst.row_begin && r < A.dst.row_end) {
             p = const_cast<uint8_t *>(A.dst.base) + uint64_t(r - A.dst.row_begin) * A.dst.stride;
             if constexpr (REVEAL) {
-                if (rinfo[j] & 0x10000u) gf_mul4(l, h, tab + j * 20u);
+                if (rinfo[j] & 0x10000u) gf_mul4(l, h, tabV + j * 20u);
                 else p = nullptr;
             }
         }
         if (p && c.pk_ok) {
-            *reinterpret_cast<uint32_t *>(p + c.pk_off) = l;
-            *reinterpret_cast<uint32_t *>(p + c.pk_off + 32) = h;
+            st32<COH>(p + c.pk_off, l);
+            st32<COH>(p + c.pk_off + 32, h);
         }
     });
 }
 
-// One butterfly layer on local bit B (global bit a + B), rows held in phase PB.
-template <int K, int LR, bool PB, int B, bool IFFT>
+// One butterfly layer on local bit B (global bit a + B), rows in phase PH.
+template <int K, int LR, int SPL, int PH, int B, bool IFFT>
 __device__ __forceinline__ void layer(const Ctx &c, const uint32_t *tab, uint32_t (&lo)[1 << LR],
                                       uint32_t (&hi)[1 << LR]) {
-    using P = Pass<K, LR>;
-    constexpr int RB = PB && P::W > 1 ? B - (K - LR) : B;  // register bit
+    using P = Pass<K, LR, SPL>;
+    constexpr int RB = B - P::start(PH);  // register bit
     static_assert(RB >= 0 && RB < LR, "bit not resident in this phase");
-    // Butterfly groups of this layer held by the lane: register index bits
-    // above RB.  One 20-word table per group, read from LDS once and used for
-    // the group's 2^RB butterflies.  The table's address is tied (empty asm)
-    // to the previous group's result, so at most one table is in flight:
-    // otherwise the compiler hoists every table of the layer and spills.
+    // Butterfly groups held by the lane: register index bits above RB.  One
+    // 20-word table per group, read from LDS once for its 2^RB butterflies.
     uint32_t dep = 0;
     static_for<0, (P::R >> (RB + 1))>([&](auto gc) {
         constexpr int i0 = decltype(gc)::value << (RB + 1);
-        uint32_t off = tw_slot<K>(B, P::template lrow<PB>(c.w, i0)) * 20u;
-        asm volatile("" : "+s"(off) : "v"(dep));
+        uint32_t off = tw_slot<K>(B, P::template lrow<PH>(c.g, i0)) * 20u;
+        if constexpr (P::kChain) {  // one table in flight
+            if constexpr (P::kUniform) asm volatile("" : "+s"(off) : "v"(dep));
+            else asm volatile("" : "+v"(off) : "v"(dep));
+        }
         const uint4 *t4 = reinterpret_cast<const uint4 *>(tab + off);
         uint32_t t[20];
 #pragma unroll
@@ -255,11 +370,7 @@ __device__ __forceinline__ void layer(const Ctx &c, const uint32_t *tab, uint32_
         static_for<0, (1 << RB)>([&](auto lc) {
             constexpr int i = i0 | decltype(lc)::value;
             constexpr int i2 = i | (1 << RB);
-            // The butterflies are independent; left alone the compiler
-            // interleaves all of them (~18 live VGPRs each) and spills.  Tie
-            // each one's inputs to the previous one's output: one butterfly
-            // in flight per wave, the other waves of the SIMD fill the gaps.
-            asm volatile("" : "+v"(lo[i]), "+v"(hi[i]), "+v"(lo[i2]), "+v"(hi[i2]) : "v"(dep));
+            if constexpr (P::kChain) asm volatile("" : "+v"(lo[i]), "+v"(hi[i]), "+v"(lo[i2]), "+v"(hi[i2]) : "v"(dep));
             if constexpr (IFFT) ifft_bfly(lo[i], hi[i], lo[i2], hi[i2], t);
             else fft_bfly(lo[i], hi[i], lo[i2], hi[i2], t);
             dep = lo[i];
@@ -267,99 +378,105 @@ __device__ __forceinline__ void layer(const Ctx &c, const uint32_t *tab, uint32_
     });
 }
 
-// Move the rows from phase FROM_B to phase TO_B through LDS, one plane at a time.
-template <int K, int LR, bool FROM_B, bool TO_B>
+// Move the rows from phase FROM to phase TO through LDS (both planes at once).
+template <int K, int LR, int SPL, int FROM, int TO>
 __device__ __forceinline__ void exchange(const Ctx &c, uint32_t *plane, uint32_t (&lo)[1 << LR],
                                          uint32_t (&hi)[1 << LR]) {
-    using P = Pass<K, LR>;
-    if constexpr (P::W == 1 || FROM_B == TO_B) return;
-    auto one = [&](uint32_t(&v)[1 << LR]) {
-        __syncthreads();
-        static_for<0, P::R>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            plane[P::template lrow<FROM_B>(c.w, i) * kLanes + c.lane] = v[i];
-        });
-        __syncthreads();
-        static_for<0, P::R>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            v[i] = plane[P::template lrow<TO_B>(c.w, i) * kLanes + c.lane];
-        });
-    };
-    one(lo);
-    one(hi);
-}
-
-// Formal derivative restricted to the set's local bits, plane by plane:
-//   x[q] <- (mode 2 ? x[q] : 0) ^ XOR_{b < K, q_b = 0} x[q | 2^b]
-template <int K, int LR, bool PB>
-__device__ __forceinline__ void formal_derivative(const Ctx &c, uint32_t mode, uint32_t *plane,
-                                                  uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
-    using P = Pass<K, LR>;
-    auto one = [&](uint32_t(&v)[1 << LR]) {
-        __syncthreads();
-        static_for<0, P::R>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            plane[P::template lrow<PB>(c.w, i) * kLanes + c.lane] = v[i];
-        });
-        __syncthreads();
-        static_for<0, P::R>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            const uint32_t j = P::template lrow<PB>(c.w, i);
-            uint32_t acc = mode == 2 ? v[i] : 0u;
-#pragma unroll
-            for (int b = 0; b < K; ++b)
-                if (!(j & (1u << b))) acc ^= plane[(j | (1u << b)) * kLanes + c.lane];
-            v[i] = acc;
-            asm volatile("" ::: "memory");
-        });
-    };
-    one(lo);
-    one(hi);
-}
-
-template <int K, int LR, bool PB>
-__device__ __forceinline__ void xor_rows_in(const PassArgs &A, const Ctx &c, uint32_t (&lo)[1 << LR],
-                                            uint32_t (&hi)[1 << LR]) {
-    using P = Pass<K, LR>;
+    using P = Pass<K, LR, SPL>;
+    constexpr uint32_t kPlane = uint32_t(P::SP) << K;
+    if constexpr (FROM == TO) return;
+    __syncthreads();
     static_for<0, P::R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        uint32_t r = c.grow(P::template lrow<PB>(c.w, i), K);
-        r = __builtin_amdgcn_readfirstlane(r);
-        asm volatile("" : "+s"(r));
-        const uint8_t *p = A.xor_in + uint64_t(r) * A.work_stride;
-        if (c.pk_ok) {
-            lo[i] ^= *reinterpret_cast<const uint32_t *>(p + c.pk_off);
-            hi[i] ^= *reinterpret_cast<const uint32_t *>(p + c.pk_off + 32);
-        }
+        const uint32_t x = P::template lrow<FROM>(c.g, i) * P::SP + c.p;
+        plane[x] = lo[i];
+        plane[kPlane + x] = hi[i];
+    });
+    __syncthreads();
+    static_for<0, P::R>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const uint32_t x = P::template lrow<TO>(c.g, i) * P::SP + c.p;
+        lo[i] = plane[x];
+        hi[i] = plane[kPlane + x];
     });
 }
 
-template <int K, int LR, bool IFFT>
-__device__ __forceinline__ void transform(const Ctx &c, uint32_t *plane, const uint32_t *tab,
-                                          uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
-    using P = Pass<K, LR>;
-    constexpr bool HAS_B = P::W > 1;
-    if constexpr (IFFT) {  // bits ascending: A-phase [0, LR), B-phase [LR, K)
-        static_for<0, (LR < K ? LR : K)>([&](auto bc) { layer<K, LR, false, decltype(bc)::value, true>(c, tab, lo, hi); });
-        if constexpr (HAS_B) {
-            exchange<K, LR, false, true>(c, plane, lo, hi);
-            static_for<LR, K>([&](auto bc) { layer<K, LR, true, decltype(bc)::value, true>(c, tab, lo, hi); });
-        }
-    } else {  // bits descending: B-phase [LR, K), A-phase [0, LR)
-        if constexpr (HAS_B) {
-            static_for<0, K - LR>([&](auto bc) { layer<K, LR, true, K - 1 - decltype(bc)::value, false>(c, tab, lo, hi); });
-            exchange<K, LR, true, false>(c, plane, lo, hi);
-        }
-        static_for<0, (LR < K ? LR : K)>([&](auto bc) {
-            constexpr int b = (LR < K ? LR : K) - 1 - decltype(bc)::value;
-            layer<K, LR, false, b, false>(c, tab, lo, hi);
-        });
-    }
+// Formal derivative restricted to the set's local bits:
+//   x[q] <- (mode 2 ? x[q] : 0) ^ XOR_{b < K, q_b = 0} x[q | 2^b]
+template <int K, int LR, int SPL, int PH>
+__device__ __forceinline__ void formal_derivative(const Ctx &c, uint32_t mode, uint32_t *plane,
+                                                  uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
+    using P = Pass<K, LR, SPL>;
+    constexpr uint32_t kPlane = uint32_t(P::SP) << K;
+    __syncthreads();
+    static_for<0, P::R>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const uint32_t x = P::template lrow<PH>(c.g, i) * P::SP + c.p;
+        plane[x] = lo[i];
+        plane[kPlane + x] = hi[i];
+    });
+    __syncthreads();
+    static_for<0, P::R>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const uint32_t j = P::template lrow<PH>(c.g, i);
+        uint32_t al = mode == 2 ? lo[i] : 0u, ah = mode == 2 ? hi[i] : 0u;
+#pragma unroll
+        for (int b = 0; b < K; ++b)
+            if (!(j & (1u << b))) {
+                const uint32_t x = (j | (1u << b)) * P::SP + c.p;
+                al ^= plane[x];
+                ah ^= plane[kPlane + x];
+            }
+        lo[i] = al;
+        hi[i] = ah;
+    });
 }
 
-template <int K, int LR, int FLAGS>
-__global__ void __launch_bounds__(kLanes << (K - LR), 2) k_pass(const PassArgs A) {
-    using P = Pass<K, LR>;
+template <int K, int LR, int SPL, int PH, bool COH>
+__device__ __forceinline__ void load_xor_rows(const PassArgs &A, const Ctx &c, uint32_t (&lo)[1 << LR],
+                                              uint32_t (&hi)[1 << LR]) {
+    using P = Pass<K, LR, SPL>;
+    static_for<0, P::R>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const uint32_t r = pin<P::kUniform>(c.grow(P::template lrow<PH>(c.g, i), K));
+        const uint8_t *p = A.xor_in + uint64_t(r) * A.work_stride;
+        uint32_t l = 0, h = 0;
+        if (c.pk_ok) {
+            l = ld32<COH>(p + c.pk_off);
+            h = ld32<COH>(p + c.pk_off + 32);
+        }
+        lo[i] = l;
+        hi[i] = h;
+    });
+}
+
+// IFFT: bits ascending, starting in phase 0, ending in phase NPH-1.
+// FFT: bits descending, starting in phase NPH-1, ending in phase 0.
+template <int K, int LR, int SPL, bool IFFT>
+__device__ __forceinline__ void transform(const Ctx &c, uint32_t *plane, const uint32_t *tab,
+                                          uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
+    using P = Pass<K, LR, SPL>;
+#ifdef RS_PROBE_SKIP_XFORM  // tools/pass_probe.hip: time a pass without its layers
+    return;
+#endif
+    static_for<0, K>([&](auto bc) {
+        constexpr int n = decltype(bc)::value;
+        constexpr int b = IFFT ? n : K - 1 - n;
+        constexpr int prev = IFFT ? b - 1 : b + 1;
+        constexpr int ph = P::phase_of(b);
+        if constexpr (n > 0 && P::phase_of(prev) != ph)
+            exchange<K, LR, SPL, P::phase_of(prev), ph>(c, plane, lo, hi);
+        layer<K, LR, SPL, ph, b, IFFT>(c, tab, lo, hi);
+    });
+}
+
+// One pass over workgroup-block (bx = set * slices + slice, by = chunk).
+// COH_LD / COH_ST: work-buffer rows are handed between workgroups of one
+// launch (k_chain phases), so they are read / written coherently.
+template <int K, int LR, int SPL, int FLAGS, bool COH_LD, bool COH_ST, int STAMP = -1>
+__device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32_t by, uint32_t *lds) {
+    using P = Pass<K, LR, SPL>;
+    using L = Lds<K, SPL, FLAGS>;
     constexpr bool DO_IFFT = FLAGS & kIfft;
     constexpr bool DO_FFT = FLAGS & kFft;
     constexpr bool MULTI_IN = FLAGS & kMultiIn;    // XOR-fold IFFTs of A.in_chunks chunks
@@ -368,95 +485,111 @@ __global__ void __launch_bounds__(kLanes << (K - LR), 2) k_pass(const PassArgs A
     constexpr bool FD = FLAGS & kFd;               // decode: formal derivative over local bits
     constexpr bool XOR_IN = FLAGS & kXorIn;        // decode: x ^= rows of A.xor_in
     constexpr bool REVEAL = FLAGS & kReveal;       // decode: store erased originals, unscaled
-    constexpr bool HAS_B = P::W > 1;
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    static_assert(!(SCALE && MULTI_IN) && !(REVEAL && MULTI_OUT), "unsupported combination");
+    constexpr int PL = P::NPH - 1;  // phase after an IFFT / before an FFT
     uint32_t *plane = lds;
-    uint32_t *tab = lds + Lds<K>::kPlane;
-    uint32_t *rinfo = tab + Lds<K>::kTab;
+    uint32_t *tabI = lds + L::oI, *tabF = lds + L::oF, *tabS = lds + L::oS, *tabV = lds + L::oV;
+    uint32_t *rinfo = lds + L::oR;
 
     Ctx c;
-    c.lane = threadIdx.x & (kLanes - 1);
-    c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t slice = blockIdx.x % A.slices;
-    const uint32_t set = blockIdx.x / A.slices;
-    const uint32_t gchunk = blockIdx.y;
+    c.p = threadIdx.x & (P::SP - 1);
+    c.g = threadIdx.x >> SPL;
+    if constexpr (P::kUniform) c.g = __builtin_amdgcn_readfirstlane(c.g);
+    const uint32_t slice = bx % A.slices;
+    const uint32_t set = bx / A.slices;
+    const uint32_t gchunk = by;
     c.a = A.a;
     c.s_lo = set & ((1u << A.a) - 1u);
     c.s_hi = set >> A.a;
-    const uint32_t pk = slice * kLanes + c.lane;
+    const uint32_t pk = slice * P::SP + c.p;
     c.pk_ok = pk < A.packs;
     c.pk_off = (pk >> 3) * 64u + (pk & 7u) * 4u;
 
     uint32_t lo[P::R], hi[P::R];
+    uint32_t xl[XOR_IN ? P::R : 1], xh[XOR_IN ? P::R : 1];
+    // loads first, then table staging: one barrier covers both latencies
+    load_rows<K, LR, SPL, DO_IFFT ? 0 : PL, SCALE, COH_LD>(A, c, gchunk, lo, hi);
+    if constexpr (XOR_IN) load_xor_rows<K, LR, SPL, PL, COH_LD>(A, c, xl, xh);
+    if constexpr (K > 0)
+        stage<K, P::kThreads>(A, c, gchunk, DO_IFFT ? tabI : nullptr, A.ifft_delta + gchunk * A.ifft_delta_step,
+                 DO_FFT && !MULTI_OUT ? tabF : nullptr, A.fft_delta + gchunk * A.fft_delta_step,
+                 SCALE ? tabS : nullptr, REVEAL ? tabV : nullptr, rinfo);
+    else
+        stage<K, P::kThreads>(A, c, gchunk, nullptr, 0, nullptr, 0, SCALE ? tabS : nullptr, REVEAL ? tabV : nullptr, rinfo);
+    __syncthreads();
+    if constexpr (STAMP >= 0) RS_STAMP(STAMP);
+    if constexpr (SCALE) scale_rows<K, LR, SPL, 0>(c, tabS, lo, hi);
 
-    // ---- load (+ IFFT per input chunk, XOR-accumulated) ------------------
-    if constexpr (DO_IFFT && !MULTI_IN) {
-        if constexpr (SCALE) stage_rows<K>(A, c, gchunk, false, tab, rinfo);
-        load_rows<K, LR, false, SCALE>(A, c, gchunk, tab, rinfo, lo, hi);
-        if constexpr (K > 0) stage_twiddles<K>(A, c, A.ifft_delta + gchunk * A.ifft_delta_step, tab);
-        transform<K, LR, true>(c, plane, tab, lo, hi);
-    } else if constexpr (DO_IFFT) {
-        uint32_t tl[P::R], th[P::R];
-        for (uint32_t ci = 0; ci < A.in_chunks; ++ci) {
-            const uint32_t chunk = gchunk + ci;
-            if constexpr (SCALE) stage_rows<K>(A, c, chunk, false, tab, rinfo);
-            load_rows<K, LR, false, SCALE>(A, c, chunk, tab, rinfo, tl, th);
-            if constexpr (K > 0) stage_twiddles<K>(A, c, A.ifft_delta + chunk * A.ifft_delta_step, tab);
-            transform<K, LR, true>(c, plane, tab, tl, th);
-            if (ci == 0) {
-                static_for<0, P::R>([&](auto ic) { lo[ic] = tl[ic]; hi[ic] = th[ic]; });
-            } else {
+    if constexpr (DO_IFFT) {
+        transform<K, LR, SPL, true>(c, plane, tabI, lo, hi);
+        if constexpr (MULTI_IN) {
+            for (uint32_t ci = 1; ci < A.in_chunks; ++ci) {
+                const uint32_t chunk = gchunk + ci;
+                uint32_t tl[P::R], th[P::R];
+                load_rows<K, LR, SPL, 0, false, COH_LD>(A, c, chunk, tl, th);
+                __syncthreads();
+                if constexpr (K > 0)
+                    stage<K, P::kThreads>(A, c, chunk, tabI, A.ifft_delta + chunk * A.ifft_delta_step, nullptr, 0, nullptr, nullptr,
+                             nullptr);
+                __syncthreads();
+                transform<K, LR, SPL, true>(c, plane, tabI, tl, th);
                 static_for<0, P::R>([&](auto ic) { lo[ic] ^= tl[ic]; hi[ic] ^= th[ic]; });
             }
         }
-    } else {
-        if constexpr (SCALE) stage_rows<K>(A, c, gchunk, false, tab, rinfo);
-        load_rows<K, LR, HAS_B, SCALE>(A, c, gchunk, tab, rinfo, lo, hi);
     }
-    // rows are now in phase B (if the pass has one)
+    // rows are now in phase PL
 
-    if constexpr (FD) formal_derivative<K, LR, HAS_B>(c, A.fd_mode, plane, lo, hi);
-    if constexpr (XOR_IN) xor_rows_in<K, LR, HAS_B>(A, c, lo, hi);
+    if constexpr (FD) formal_derivative<K, LR, SPL, PL>(c, A.fd_mode, plane, lo, hi);
+    if constexpr (XOR_IN) static_for<0, P::R>([&](auto ic) { lo[ic] ^= xl[ic]; hi[ic] ^= xh[ic]; });
 
-    // ---- FFT per output chunk + store ------------------------------------
     if constexpr (DO_FFT && !MULTI_OUT) {
-        if constexpr (K > 0) stage_twiddles<K>(A, c, A.fft_delta + gchunk * A.fft_delta_step, tab);
-        transform<K, LR, false>(c, plane, tab, lo, hi);
-        if constexpr (REVEAL) stage_rows<K>(A, c, gchunk, true, tab, rinfo);
-        store_rows<K, LR, false, REVEAL>(A, c, gchunk, tab, rinfo, lo, hi);
+        transform<K, LR, SPL, false>(c, plane, tabF, lo, hi);
+        if constexpr (STAMP >= 0) RS_STAMP(STAMP + 1);
+        store_rows<K, LR, SPL, 0, REVEAL, COH_ST>(A, c, gchunk, tabV, rinfo, lo, hi);
     } else if constexpr (DO_FFT) {
         for (uint32_t co = 0; co < A.out_chunks; ++co) {
             const uint32_t chunk = gchunk + co;
             uint32_t yl[P::R], yh[P::R];
             static_for<0, P::R>([&](auto ic) { yl[ic] = lo[ic]; yh[ic] = hi[ic]; });
-            if constexpr (K > 0) stage_twiddles<K>(A, c, A.fft_delta + chunk * A.fft_delta_step, tab);
-            transform<K, LR, false>(c, plane, tab, yl, yh);
-            if constexpr (REVEAL) stage_rows<K>(A, c, chunk, true, tab, rinfo);
-            store_rows<K, LR, false, REVEAL>(A, c, chunk, tab, rinfo, yl, yh);
+            __syncthreads();
+            if constexpr (K > 0)
+                stage<K, P::kThreads>(A, c, chunk, nullptr, 0, tabF, A.fft_delta + chunk * A.fft_delta_step, nullptr, nullptr,
+                         nullptr);
+            __syncthreads();
+            transform<K, LR, SPL, false>(c, plane, tabF, yl, yh);
+            store_rows<K, LR, SPL, 0, false, COH_ST>(A, c, chunk, tabV, rinfo, yl, yh);
         }
     } else {
-        if constexpr (REVEAL) stage_rows<K>(A, c, gchunk, true, tab, rinfo);
-        store_rows<K, LR, HAS_B, REVEAL>(A, c, gchunk, tab, rinfo, lo, hi);
+        if constexpr (STAMP >= 0) RS_STAMP(STAMP + 1);
+        store_rows<K, LR, SPL, PL, REVEAL, COH_ST>(A, c, gchunk, tabV, rinfo, lo, hi);
     }
 }
 
-template <int K, int LR, int F>
+template <int K, int LR, int SPL, int FLAGS>
+__global__ void __launch_bounds__(1 << (K - LR + SPL), 2) k_pass(const PassArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    pass_body<K, LR, SPL, FLAGS, false, false>(A, blockIdx.x, blockIdx.y, lds);
+}
+
+template <int K, int LR, int SPL, int F>
 hipError_t launch_f(const PassArgs &A, hipStream_t s) {
-    using P = Pass<K, LR>;
-    const size_t lds = Lds<K>::bytes();
+    using P = Pass<K, LR, SPL>;
+    const size_t lds = Lds<K, SPL, F>::bytes();
     static bool attr_set = false;  // benign race: idempotent attribute call
     if (!attr_set && lds > 65536) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pass<K, LR, F>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pass<K, LR, SPL, F>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    dim3 grid(A.slices * A.nsets, A.grid_chunks);
-    k_pass<K, LR, F><<<grid, P::kThreads, lds, s>>>(A);
+    PassArgs B = A;
+    B.slices = (A.packs + P::SP - 1) / P::SP;
+    dim3 grid(B.slices * B.nsets, B.grid_chunks);
+    k_pass<K, LR, SPL, F><<<grid, P::kThreads, lds, s>>>(B);
     return hipGetLastError();
 }
 
-template <int K, int LR>
+template <int K, int LR, int SPL>
 hipError_t launch_k(int flags, const PassArgs &A, hipStream_t s) {
     if (A.in_chunks > 1) flags |= kMultiIn;
     if (A.out_chunks > 1) flags |= kMultiOut;
@@ -467,20 +600,170 @@ hipError_t launch_k(int flags, const PassArgs &A, hipStream_t s) {
     constexpr int I = kIfft, F = kFft;
     switch (flags) {
         // encode / engine
-        case I: return launch_f<K, LR, I>(A, s);
-        case F: return launch_f<K, LR, F>(A, s);
-        case I | F: return launch_f<K, LR, I | F>(A, s);
-        case I | kMultiIn: return launch_f<K, LR, I | kMultiIn>(A, s);
-        case I | F | kMultiIn: return launch_f<K, LR, I | F | kMultiIn>(A, s);
-        case I | F | kMultiOut: return launch_f<K, LR, I | F | kMultiOut>(A, s);
-        case F | kMultiOut: return launch_f<K, LR, F | kMultiOut>(A, s);
+        case I: return launch_f<K, LR, SPL, I>(A, s);
+        case F: return launch_f<K, LR, SPL, F>(A, s);
+        case I | F: return launch_f<K, LR, SPL, I | F>(A, s);
+        case I | kMultiIn: return launch_f<K, LR, SPL, I | kMultiIn>(A, s);
+        case I | F | kMultiIn: return launch_f<K, LR, SPL, I | F | kMultiIn>(A, s);
+        case I | F | kMultiOut: return launch_f<K, LR, SPL, I | F | kMultiOut>(A, s);
+        case F | kMultiOut: return launch_f<K, LR, SPL, F | kMultiOut>(A, s);
         // decode: single pass, IFFT passes, fused top, FFT passes (middle / last)
-        case I | F | kScale | kFd | kReveal: return launch_f<K, LR, I | F | kScale | kFd | kReveal>(A, s);
-        case I | kScale: return launch_f<K, LR, I | kScale>(A, s);
-        case I | F | kFd: return launch_f<K, LR, I | F | kFd>(A, s);
-        case F | kFd | kXorIn: return launch_f<K, LR, F | kFd | kXorIn>(A, s);
-        case F | kFd | kXorIn | kReveal: return launch_f<K, LR, F | kFd | kXorIn | kReveal>(A, s);
+        case I | F | kScale | kFd | kReveal: return launch_f<K, LR, SPL, I | F | kScale | kFd | kReveal>(A, s);
+        case I | kScale: return launch_f<K, LR, SPL, I | kScale>(A, s);
+        case I | F | kFd: return launch_f<K, LR, SPL, I | F | kFd>(A, s);
+        case F | kFd | kXorIn: return launch_f<K, LR, SPL, F | kFd | kXorIn>(A, s);
+        case F | kFd | kXorIn | kReveal: return launch_f<K, LR, SPL, F | kFd | kXorIn | kReveal>(A, s);
         default: return hipErrorInvalidValue;
+    }
+}
+
+// Two shapes per K: "wide" (64-pack slices, 8 rows per lane) for matrices
+// that fill the chip, "narrow" (16..32-pack slices, 2..4 rows per lane) to
+// spread small matrices over more workgroups and waves.
+template <int K>
+hipError_t launch_shape(bool narrow, int flags, const PassArgs &A, hipStream_t s) {
+    constexpr int LRW = K < 3 ? K : 3;
+    if constexpr (K >= 2) {
+        constexpr int LRN = K < 3 ? 1 : 2;
+        constexpr int SPLN = 6 - (K - LRN) > 4 ? 6 - (K - LRN) : 4;
+        if (narrow) return launch_k<K, LRN, SPLN>(flags, A, s);
+    }
+    return launch_k<K, LRW, 6>(flags, A, s);
+}
+
+
+// ---------------------------------------------------------------------------
+// Chain kernel: the three passes of a 2-level transform (level 0, fused top
+// level 1, level 0) in ONE launch.  Columns are independent, so only the
+// workgroups of one column slice exchange rows; they meet at a barrier after
+// phases 0 and 1 (write-through row stores, vmcnt(0), workgroup barrier,
+// one agent-scope counter add per workgroup, a coherent poll; rows are read
+// back coherently).  Launch boundaries cost ~1.5 us of GPU time plus ~2-3 us
+// of host enqueue each; a slice barrier ~1 us.  All workgroups must be
+// co-resident: the host sizes the grid far below capacity, and every wait is
+// bounded (a timed-out wait sets *fault instead of hanging the device).
+constexpr uint32_t kSpinLimit = 1u << 21;
+
+__device__ __forceinline__ void slice_barrier(uint32_t *ctr, uint32_t members, uint32_t *fault) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t spins = 0;
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < members) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > kSpinLimit) {
+                __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// Row-group bits of a chain workgroup: equal in both levels (the block size
+// is fixed), LR = K - GB rows per lane.
+template <int K1, int SPL>
+constexpr int chain_gb() {
+    return K1 - 1 < 10 - SPL ? K1 - 1 : 10 - SPL;
+}
+
+template <int MODE>
+struct ChainFlags;
+template <>
+struct ChainFlags<kChainEncodeHigh> {
+    static constexpr int F0 = kIfft, F1 = kIfft | kFft | kMultiIn, F2 = kFft;
+};
+template <>
+struct ChainFlags<kChainEncodeLow> {
+    static constexpr int F0 = kIfft, F1 = kIfft | kFft | kMultiOut, F2 = kFft;
+};
+template <>
+struct ChainFlags<kChainDecode> {
+    static constexpr int F0 = kIfft | kScale, F1 = kIfft | kFft | kFd, F2 = kFft | kFd | kXorIn | kReveal;
+};
+
+template <int K, int LR, int SPL, int FLAGS, bool COH_LD, bool COH_ST, int STAMP>
+__device__ __forceinline__ void chain_phase(const ChainArgs &C, const PassArgs &A, uint32_t items, uint32_t slice,
+                                            uint32_t q, uint32_t *lds) {
+    for (uint32_t it = q; it < items; it += C.members) {
+        if (it != q) __syncthreads();  // the previous item's LDS readers are done
+        const uint32_t set = it % A.nsets, chunk = it / A.nsets;
+        pass_body<K, LR, SPL, FLAGS, COH_LD, COH_ST, STAMP>(A, set * A.slices + slice, chunk, lds);
+    }
+}
+
+template <int K0, int K1, int SPL, int MODE>
+__global__ void __launch_bounds__(1 << (chain_gb<K1, SPL>() + SPL)) k_chain(const ChainArgs C) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    constexpr int GB = chain_gb<K1, SPL>();
+    using Fl = ChainFlags<MODE>;
+    const uint32_t nsl = C.ph[0].slices;
+    const uint32_t slice = blockIdx.x % nsl, q = blockIdx.x / nsl;
+    uint32_t *ctr = C.sync + slice * 32u;
+    RS_STAMP(0);
+    chain_phase<K0, K0 - GB, SPL, Fl::F0, false, true, 8>(C, C.ph[0], C.items[0], slice, q, lds);
+    RS_STAMP(1);
+    slice_barrier(ctr, C.members, C.fault);
+    RS_STAMP(2);
+    chain_phase<K1, K1 - GB, SPL, Fl::F1, true, true, 10>(C, C.ph[1], C.items[1], slice, q, lds);
+    RS_STAMP(3);
+    slice_barrier(ctr + 1, C.members, C.fault);
+    RS_STAMP(4);
+    chain_phase<K0, K0 - GB, SPL, Fl::F2, true, false, 12>(C, C.ph[2], C.items[2], slice, q, lds);
+    RS_STAMP(5);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    RS_STAMP(6);
+    // Leave the counters zero for the next launch: the last workgroup out
+    // (every member has passed both waits) resets them.
+    if (threadIdx.x == 0) {
+        const uint32_t out = __hip_atomic_fetch_add(ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (out == C.members - 1) {
+            __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ctr + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+template <int K0, int K1, int SPL, int MODE>
+hipError_t launch_chain_f(const ChainArgs &C, hipStream_t s) {
+    constexpr int GB = chain_gb<K1, SPL>();
+    using Fl = ChainFlags<MODE>;
+    constexpr size_t l0 = Lds<K0, SPL, Fl::F0>::bytes(), l1 = Lds<K1, SPL, Fl::F1>::bytes(),
+                     l2 = Lds<K0, SPL, Fl::F2>::bytes();
+    constexpr size_t lds = l0 > l1 ? (l0 > l2 ? l0 : l2) : (l1 > l2 ? l1 : l2);
+    static bool attr_set = false;
+    if (!attr_set && lds > 65536) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_chain<K0, K1, SPL, MODE>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    k_chain<K0, K1, SPL, MODE><<<dim3(C.ph[0].slices * C.members), 1 << (GB + SPL), lds, s>>>(C);
+    return hipGetLastError();
+}
+
+template <int K0, int K1, int MODE>
+hipError_t launch_chain_s(int spl, const ChainArgs &C, hipStream_t s) {
+    switch (spl) {
+        case 4: return launch_chain_f<K0, K1, 4, MODE>(C, s);
+        case 5: return launch_chain_f<K0, K1, 5, MODE>(C, s);
+        case 6: return launch_chain_f<K0, K1, 6, MODE>(C, s);
+        default: return hipErrorNotSupported;
+    }
+}
+
+template <int MODE>
+hipError_t launch_chain_m(int K0, int K1, int spl, const ChainArgs &C, hipStream_t s) {
+    switch (K0 * 8 + K1) {
+        case 4 * 8 + 3: return launch_chain_s<4, 3, MODE>(spl, C, s);
+        case 4 * 8 + 4: return launch_chain_s<4, 4, MODE>(spl, C, s);
+        case 5 * 8 + 4: return launch_chain_s<5, 4, MODE>(spl, C, s);
+        case 5 * 8 + 5: return launch_chain_s<5, 5, MODE>(spl, C, s);
+        case 6 * 8 + 5: return launch_chain_s<6, 5, MODE>(spl, C, s);
+        case 6 * 8 + 6: return launch_chain_s<6, 6, MODE>(spl, C, s);
+        default: return hipErrorNotSupported;
     }
 }
 
@@ -557,15 +840,27 @@ __global__ void k_formal_derivative(const uint8_t *in, uint8_t *out, uint32_t ro
 }  // namespace
 
 hipError_t launch_pass(int K, int flags, const PassArgs &A, hipStream_t s) {
+    // narrow slices when 64-pack slices leave the chip under-filled
+    const uint64_t wide_groups = uint64_t(A.nsets) * ((A.packs + 63) / 64) * A.grid_chunks;
+    const bool narrow = wide_groups < 1024;
     switch (K) {
-        case 0: return launch_k<0, 0>(flags, A, s);
-        case 1: return launch_k<1, 1>(flags, A, s);
-        case 2: return launch_k<2, 1>(flags, A, s);
-        case 3: return launch_k<3, 2>(flags, A, s);
-        case 4: return launch_k<4, 2>(flags, A, s);
-        case 5: return launch_k<5, 3>(flags, A, s);
-        case 6: return launch_k<6, 3>(flags, A, s);
+        case 0: return launch_shape<0>(narrow, flags, A, s);
+        case 1: return launch_shape<1>(narrow, flags, A, s);
+        case 2: return launch_shape<2>(narrow, flags, A, s);
+        case 3: return launch_shape<3>(narrow, flags, A, s);
+        case 4: return launch_shape<4>(narrow, flags, A, s);
+        case 5: return launch_shape<5>(narrow, flags, A, s);
+        case 6: return launch_shape<6>(narrow, flags, A, s);
         default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_chain(int mode, int K0, int K1, int spl, const ChainArgs &C, hipStream_t s) {
+    switch (mode) {
+        case kChainEncodeHigh: return launch_chain_m<kChainEncodeHigh>(K0, K1, spl, C, s);
+        case kChainEncodeLow: return launch_chain_m<kChainEncodeLow>(K0, K1, spl, C, s);
+        case kChainDecode: return launch_chain_m<kChainDecode>(K0, K1, spl, C, s);
+        default: return hipErrorNotSupported;
     }
 }
 

@@ -118,6 +118,24 @@ def profile_collect(ctx=None, max_records: int = 1 << 16):
     n = _lib.rs_profile_collect(ctx.handle, ms, by, nm, max_records)
     return [(nm[i].decode(), float(ms[i]), int(by[i])) for i in range(max(n, 0))]
 
+
+_sig("rs_chain_enable", _int, _vp, _int)
+_sig("rs_check_device", _int, _vp)
+
+
+def chain_enable(enable: bool = True, ctx=None) -> None:
+    """Allow (default) or forbid the one-launch chain kernel for small transforms."""
+    ctx = ctx or default_context()
+    _lib.rs_chain_enable(ctx.handle, 1 if enable else 0)
+
+
+def check_device(ctx=None) -> None:
+    """Synchronize; raise DeviceError if an in-kernel barrier wait timed out."""
+    ctx = ctx or default_context()
+    st = _lib.rs_check_device(ctx.handle)
+    if st != 0:
+        raise DeviceError(_lib.rs_last_device_error().decode())
+
 GF_BITS = 16
 GF_ORDER = 65536
 GF_MODULUS = 65535

@@ -446,3 +446,51 @@ def test_baseline_decode_8192_64k(torch, rs, loss):
     rs.decode_device(N, M, S, d_in, op, d_rec, rp, d_out)
     torch.cuda.synchronize()
     assert torch.equal(d_out[N - L:], d_orig[N - L:])
+
+
+# ---------------------------------------------------------------------------
+# chain kernel (one launch, in-kernel slice barriers) vs one launch per pass
+
+CHAIN_CASES = [
+    # 2-level transforms (2^7 .. 2^12 rows), several chunk counts and shard sizes
+    ("high", 128, 128, 64), ("high", 1024, 1024, 1024), ("high", 4000, 128, 192), ("low", 128, 4000, 192),
+    ("high", 4096, 4096, 64), ("low", 1000, 1500, 1088), ("high", 2048, 2048, 4096), ("default", 600, 200, 8192),
+]
+
+
+@pytest.mark.parametrize("chain", [True, False])
+@pytest.mark.parametrize("rate,N,M,S", CHAIN_CASES)
+def test_chain_and_pass_paths_match_oracle(torch, rs, rate, N, M, S, chain):
+    rs.chain_enable(chain)
+    try:
+        orig = O.generate_original(N, S, (N + M + S) & 0xFF)
+        want = O.encode(rate, orig, M)
+        got = gpu_encode(torch, rs, rate, orig, M)
+        assert np.array_equal(got, want)
+        rng = np.random.default_rng(N * 7 + M)
+        L = min(N, M)
+        op = np.ones(N, np.uint8)
+        op[rng.choice(N, L, replace=False)] = 0
+        rp = np.zeros(M, np.uint8)
+        rp[rng.choice(M, L, replace=False)] = 1
+        dw = O.decode(rate, orig, op, want, rp)
+        dg = gpu_decode(torch, rs, rate, orig, op, want, rp)
+        miss = op == 0
+        assert np.array_equal(dg[miss], orig[miss]) and np.array_equal(dg[miss], dw[miss])
+        rs.check_device()
+    finally:
+        rs.chain_enable(True)
+
+
+def test_chain_repeated_launches_stay_in_sync(torch, rs):
+    """Back-to-back chain launches reuse the barrier counters (reset in-kernel)."""
+    N = M = 1024
+    S = 1024
+    orig = O.generate_original(N, S, 9)
+    want = O.encode("high", orig, M)
+    d_orig = _dev(torch, orig)
+    d_rec = torch.empty((M, S), dtype=torch.uint8, device="cuda")
+    for _ in range(200):
+        rs.encode_device(N, M, S, d_orig, d_rec, rate_=1)
+    rs.check_device()
+    assert np.array_equal(d_rec.cpu().numpy(), want)
