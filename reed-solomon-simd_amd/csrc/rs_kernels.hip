@@ -450,8 +450,51 @@ __device__ __forceinline__ void load_xor_rows(const PassArgs &A, const Ctx &c, u
     });
 }
 
+// Twiddle tables of one layer held in registers: one 20-word table per
+// butterfly group of the lane (at most R/2 groups, when the layer's bit is
+// the lowest register bit).
+template <int LR>
+struct LayerTabs {
+    uint32_t w[(1 << LR) / 2][20];
+};
+
+template <int K, int LR, int SPL, int PH, int B>
+__device__ __forceinline__ void read_tables(const Ctx &c, const uint32_t *tab, LayerTabs<LR> &T) {
+    using P = Pass<K, LR, SPL>;
+    constexpr int RB = B - P::start(PH);
+    static_for<0, (P::R >> (RB + 1))>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        const uint32_t off = tw_slot<K>(B, P::template lrow<PH>(c.g, g << (RB + 1))) * 20u;
+        const uint4 *t4 = reinterpret_cast<const uint4 *>(tab + off);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const uint4 v = t4[q];
+            T.w[g][4 * q] = v.x, T.w[g][4 * q + 1] = v.y, T.w[g][4 * q + 2] = v.z, T.w[g][4 * q + 3] = v.w;
+        }
+    });
+}
+
+template <int K, int LR, int SPL, int PH, int B, bool IFFT>
+__device__ __forceinline__ void apply_layer(const LayerTabs<LR> &T, uint32_t (&lo)[1 << LR],
+                                            uint32_t (&hi)[1 << LR]) {
+    using P = Pass<K, LR, SPL>;
+    constexpr int RB = B - P::start(PH);
+    static_for<0, (P::R >> (RB + 1))>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        static_for<0, (1 << RB)>([&](auto lc) {
+            constexpr int i = (g << (RB + 1)) | decltype(lc)::value;
+            constexpr int i2 = i | (1 << RB);
+            if constexpr (IFFT) ifft_bfly(lo[i], hi[i], lo[i2], hi[i2], T.w[g]);
+            else fft_bfly(lo[i], hi[i], lo[i2], hi[i2], T.w[g]);
+        });
+    });
+}
+
 // IFFT: bits ascending, starting in phase 0, ending in phase NPH-1.
 // FFT: bits descending, starting in phase NPH-1, ending in phase 0.
+// Narrow shapes (<= 4 rows per lane) read layer n+1's tables into registers
+// while layer n runs, so the LDS latency hides behind the butterflies and
+// the phase exchanges; wide shapes read one table at a time (registers).
 template <int K, int LR, int SPL, bool IFFT>
 __device__ __forceinline__ void transform(const Ctx &c, uint32_t *plane, const uint32_t *tab,
                                           uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
@@ -459,15 +502,33 @@ __device__ __forceinline__ void transform(const Ctx &c, uint32_t *plane, const u
 #ifdef RS_PROBE_SKIP_XFORM  // tools/pass_probe.hip: time a pass without its layers
     return;
 #endif
-    static_for<0, K>([&](auto bc) {
-        constexpr int n = decltype(bc)::value;
-        constexpr int b = IFFT ? n : K - 1 - n;
-        constexpr int prev = IFFT ? b - 1 : b + 1;
-        constexpr int ph = P::phase_of(b);
-        if constexpr (n > 0 && P::phase_of(prev) != ph)
-            exchange<K, LR, SPL, P::phase_of(prev), ph>(c, plane, lo, hi);
-        layer<K, LR, SPL, ph, b, IFFT>(c, tab, lo, hi);
-    });
+    if constexpr (P::kChain || K == 0) {
+        static_for<0, K>([&](auto bc) {
+            constexpr int n = decltype(bc)::value;
+            constexpr int b = IFFT ? n : K - 1 - n;
+            constexpr int prev = IFFT ? b - 1 : b + 1;
+            constexpr int ph = P::phase_of(b);
+            if constexpr (n > 0 && P::phase_of(prev) != ph)
+                exchange<K, LR, SPL, P::phase_of(prev), ph>(c, plane, lo, hi);
+            layer<K, LR, SPL, ph, b, IFFT>(c, tab, lo, hi);
+        });
+    } else {
+        LayerTabs<LR> T[2];
+        constexpr int b0 = IFFT ? 0 : K - 1;
+        read_tables<K, LR, SPL, P::phase_of(b0), b0>(c, tab, T[0]);
+        static_for<0, K>([&](auto bc) {
+            constexpr int n = decltype(bc)::value;
+            constexpr int b = IFFT ? n : K - 1 - n;
+            constexpr int prev = IFFT ? b - 1 : b + 1;
+            constexpr int next = IFFT ? b + 1 : b - 1;
+            constexpr int ph = P::phase_of(b);
+            if constexpr (n + 1 < K)
+                read_tables<K, LR, SPL, P::phase_of(next), next>(c, tab, T[(n + 1) & 1]);
+            if constexpr (n > 0 && P::phase_of(prev) != ph)
+                exchange<K, LR, SPL, P::phase_of(prev), ph>(c, plane, lo, hi);
+            apply_layer<K, LR, SPL, ph, b, IFFT>(T[n & 1], lo, hi);
+        });
+    }
 }
 
 // One pass over workgroup-block (bx = set * slices + slice, by = chunk).
