@@ -40,6 +40,18 @@ CONFIGS = {
 }
 
 
+def reduce_max(x, world, device):
+    """Max of a per-rank scalar over all ranks (the timing contract: max over ranks)."""
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -81,11 +93,7 @@ def main():
             dist.barrier()
 
     def max_over_ranks(x):
-        if world == 1:
-            return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        return reduce_max(x, world, dev)
 
     def timed(fn, steps, warmup):
         with torch.cuda.stream(stream):

@@ -160,6 +160,20 @@ rs_status rs_decode_device(rs_context *ctx, rs_rate rate, uint64_t original_coun
                            uint64_t shard_bytes, const void *d_original, const uint8_t *original_present,
                            const void *d_recovery, const uint8_t *recovery_present, void *d_restored, void *stream,
                            rs_error *err);
+/* Column slices of wider matrices: shard r of a matrix starts at base + r * stride
+ * (stride 0 = shard_bytes; otherwise >= shard_bytes and a multiple of 4; device
+ * pointers 4-byte aligned).  Every engine op is column-wise
+ * (src/engine/utils.rs:35-43), so encoding a range of whole 64-byte blocks of
+ * each shard yields exactly those blocks of the full recovery shards: the
+ * building block of the column-partitioned multi-GPU encode. */
+rs_status rs_encode_device_strided(rs_context *ctx, rs_rate rate, uint64_t original_count, uint64_t recovery_count,
+                                   uint64_t shard_bytes, const void *d_original, uint64_t original_stride,
+                                   void *d_recovery, uint64_t recovery_stride, void *stream, rs_error *err);
+rs_status rs_decode_device_strided(rs_context *ctx, rs_rate rate, uint64_t original_count, uint64_t recovery_count,
+                                   uint64_t shard_bytes, const void *d_original, uint64_t original_stride,
+                                   const uint8_t *original_present, const void *d_recovery, uint64_t recovery_stride,
+                                   const uint8_t *recovery_present, void *d_restored, uint64_t restored_stride,
+                                   void *stream, rs_error *err);
 
 /* ---- Engine trait over a device shard matrix (src/engine.rs:234-291) ----
  * d_rows: shard_count rows of shard_len_64 64-byte blocks (ShardsRefMut,

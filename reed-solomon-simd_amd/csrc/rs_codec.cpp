@@ -171,11 +171,17 @@ void prof_end(hipStream_t s, hipEvent_t ev, const char *name, uint64_t bytes) {
 
 namespace {
 
-// Geometry of a device shard matrix: rows of `stride` bytes, `packs` packs of
-// 4 elements each (8 bytes: 4 low + 4 high) per row.
+// Geometry of a transform: `packs` packs of 4 elements each (8 bytes: 4 low +
+// 4 high) per row; work buffers use rows of `stride` bytes.  The caller's
+// matrices may be column slices of wider ones: their own row strides (0 =
+// `stride`).
 struct Geom {
     uint64_t stride;
     uint32_t packs;
+    uint64_t orig_stride = 0, rec_stride = 0, out_stride = 0;
+    uint64_t orig() const { return orig_stride ? orig_stride : stride; }
+    uint64_t rec() const { return rec_stride ? rec_stride : stride; }
+    uint64_t out() const { return out_stride ? out_stride : stride; }
 };
 
 rs::PassArgs base_args(rs_context *ctx, const Geom &g, uint32_t n) {
@@ -310,7 +316,7 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
     rs::PassArgs A = base_args(ctx, g, n);
     A.ifft_delta = n;
     A.ifft_delta_step = n;
-    const rs::RowMap src{orig, g.stride, 0, uint32_t(N)}, dst{rec, g.stride, 0, uint32_t(M)};
+    const rs::RowMap src{orig, g.orig(), 0, uint32_t(N)}, dst{rec, g.rec(), 0, uint32_t(M)};
     if (lv.m == 1) {
         A.src[0] = src;
         A.nsrc = 1;
@@ -360,7 +366,7 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
     rs::PassArgs A = base_args(ctx, g, n);
     A.fft_delta = n;
     A.fft_delta_step = n;
-    const rs::RowMap src{orig, g.stride, 0, uint32_t(N)}, dst{rec, g.stride, 0, uint32_t(M)};
+    const rs::RowMap src{orig, g.orig(), 0, uint32_t(N)}, dst{rec, g.rec(), 0, uint32_t(M)};
     if (lv.m == 1) {
         A.src[0] = src;
         A.nsrc = 1;
@@ -438,9 +444,9 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
 
     rs::PassArgs A = base_args(ctx, g, nd);
     A.rowinfo = d_rowinfo;
-    const rs::RowMap rec_map{rec, g.stride, high ? 0u : chunk, high ? uint32_t(M) : end};
-    const rs::RowMap orig_map{orig, g.stride, high ? chunk : 0u, high ? end : uint32_t(N)};
-    const rs::RowMap out_map{restored, g.stride, orig_map.row_begin, orig_map.row_end};
+    const rs::RowMap rec_map{rec, g.rec(), high ? 0u : chunk, high ? uint32_t(M) : end};
+    const rs::RowMap orig_map{orig, g.orig(), high ? chunk : 0u, high ? end : uint32_t(N)};
+    const rs::RowMap out_map{restored, g.out(), orig_map.row_begin, orig_map.row_end};
     const Levels lv = levels(u);
     if (lv.m == 1) {
         A.src[0] = rec_map;
@@ -681,16 +687,24 @@ uint64_t rs_decoder_work_count(rs_rate rate, uint64_t N, uint64_t M) {
 
 // ---- device-resident ------------------------------------------------------
 
-rs_status rs_encode_device(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, const void *d_orig,
-                           void *d_rec, void *stream, rs_error *err) {
-    if (!ctx || !d_orig || !d_rec) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+namespace {
+bool stride_ok(uint64_t stride, uint64_t S) { return stride == 0 || (stride >= S && stride % 4 == 0); }
+bool ptr_ok(const void *p) { return p && (reinterpret_cast<uintptr_t>(p) & 3) == 0; }
+}  // namespace
+
+rs_status rs_encode_device_strided(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S,
+                                   const void *d_orig, uint64_t orig_stride, void *d_rec, uint64_t rec_stride,
+                                   void *stream, rs_error *err) {
+    if (!ctx || !ptr_ok(d_orig) || !ptr_ok(d_rec)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     const int high = resolve(rate, N, M, S, err);
     if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
-    if (S % 64) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    if (S % 64 || !stride_ok(orig_stride, S) || !stride_ok(rec_stride, S)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     return guarded(err, [&]() -> rs_status {
         std::lock_guard<std::mutex> lock(ctx->mu);
         ProfScope prof(ctx);
-        const Geom g{S, uint32_t(S / 8)};
+        Geom g{S, uint32_t(S / 8)};
+        g.orig_stride = orig_stride;
+        g.rec_stride = rec_stride;
         auto s = static_cast<hipStream_t>(stream);
         if (high)
             encode_high(ctx, ctx->ws, g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
@@ -700,14 +714,21 @@ rs_status rs_encode_device(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M
     });
 }
 
-rs_status rs_decode_device(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, const void *d_orig,
-                           const uint8_t *orig_present, const void *d_rec, const uint8_t *rec_present,
-                           void *d_restored, void *stream, rs_error *err) {
-    if (!ctx || !d_orig || !d_rec || !d_restored || !orig_present || !rec_present)
+rs_status rs_encode_device(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, const void *d_orig,
+                           void *d_rec, void *stream, rs_error *err) {
+    return rs_encode_device_strided(ctx, rate, N, M, S, d_orig, 0, d_rec, 0, stream, err);
+}
+
+rs_status rs_decode_device_strided(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S,
+                                   const void *d_orig, uint64_t orig_stride, const uint8_t *orig_present,
+                                   const void *d_rec, uint64_t rec_stride, const uint8_t *rec_present,
+                                   void *d_restored, uint64_t restored_stride, void *stream, rs_error *err) {
+    if (!ctx || !ptr_ok(d_orig) || !ptr_ok(d_rec) || !ptr_ok(d_restored) || !orig_present || !rec_present)
         return set_err(err, RS_ERR_INVALID_ARGUMENT);
     const int high = resolve(rate, N, M, S, err);
     if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
-    if (S % 64) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    if (S % 64 || !stride_ok(orig_stride, S) || !stride_ok(rec_stride, S) || !stride_ok(restored_stride, S))
+        return set_err(err, RS_ERR_INVALID_ARGUMENT);
     uint64_t have_o = 0, have_r = 0;
     for (uint64_t i = 0; i < N; ++i) have_o += orig_present[i] != 0;
     for (uint64_t i = 0; i < M; ++i) have_r += rec_present[i] != 0;
@@ -720,12 +741,22 @@ rs_status rs_decode_device(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M
     return guarded(err, [&]() -> rs_status {
         std::lock_guard<std::mutex> lock(ctx->mu);
         ProfScope prof(ctx);
-        const Geom g{S, uint32_t(S / 8)};
+        Geom g{S, uint32_t(S / 8)};
+        g.orig_stride = orig_stride;
+        g.rec_stride = rec_stride;
+        g.out_stride = restored_stride;
         decode_dev(ctx, ctx->ws, high, g, N, M, static_cast<const uint8_t *>(d_orig), orig_present,
                    static_cast<const uint8_t *>(d_rec), rec_present, static_cast<uint8_t *>(d_restored),
                    static_cast<hipStream_t>(stream));
         return set_err(err, RS_OK);
     });
+}
+
+rs_status rs_decode_device(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, const void *d_orig,
+                           const uint8_t *orig_present, const void *d_rec, const uint8_t *rec_present,
+                           void *d_restored, void *stream, rs_error *err) {
+    return rs_decode_device_strided(ctx, rate, N, M, S, d_orig, 0, orig_present, d_rec, 0, rec_present, d_restored,
+                                    0, stream, err);
 }
 
 // ---- encoder ----------------------------------------------------------------

@@ -89,6 +89,9 @@ _sig("rs_decoder_is_high_rate", _int, _vp)
 _sig("rs_decoder_free", None, _vp)
 _sig("rs_encode_device", _int, _vp, _int, _u64, _u64, _u64, _vp, _vp, _vp, _E)
 _sig("rs_decode_device", _int, _vp, _int, _u64, _u64, _u64, _vp, ctypes.c_char_p, _vp, ctypes.c_char_p, _vp, _vp, _E)
+_sig("rs_encode_device_strided", _int, _vp, _int, _u64, _u64, _u64, _vp, _u64, _vp, _u64, _vp, _E)
+_sig("rs_decode_device_strided", _int, _vp, _int, _u64, _u64, _u64, _vp, _u64, ctypes.c_char_p, _vp, _u64,
+     ctypes.c_char_p, _vp, _u64, _vp, _E)
 _sig("rs_engine_fft", _int, _vp, _vp, _u64, _u64, _u64, _u64, _u64, _u64, _vp)
 _sig("rs_engine_ifft", _int, _vp, _vp, _u64, _u64, _u64, _u64, _u64, _u64, _vp)
 _sig("rs_engine_mul", _int, _vp, _vp, _u64, ctypes.c_uint16, _vp)
@@ -603,12 +606,26 @@ def _stream(stream) -> Optional[int]:
     return int(stream)
 
 
+def _row_stride(x) -> int:
+    """Row stride in bytes of a 2-D uint8 tensor view (0 = contiguous / raw pointer)."""
+    if hasattr(x, "stride") and callable(x.stride) and x.dim() == 2:
+        if x.stride(1) != 1:
+            raise ValueError("shard rows must be contiguous (stride(1) == 1)")
+        return 0 if x.is_contiguous() else int(x.stride(0)) * x.element_size()
+    return 0
+
+
 def encode_device(original_count: int, recovery_count: int, shard_bytes: int, d_original, d_recovery,
                   stream=None, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None) -> None:
+    """Encode shard matrices resident in device memory (rs_encode_device[_strided]).
+
+    d_original / d_recovery: torch uint8 tensors [count, shard_bytes] (column-slice views of wider
+    matrices allowed) or raw device pointers to contiguous rows."""
     ctx = ctx or default_context()
     err = _RsError()
-    _raise(_lib.rs_encode_device(ctx.handle, rate_, original_count, recovery_count, shard_bytes, _ptr(d_original),
-                                 _ptr(d_recovery), _stream(stream), ctypes.byref(err)), err)
+    _raise(_lib.rs_encode_device_strided(ctx.handle, rate_, original_count, recovery_count, shard_bytes,
+                                         _ptr(d_original), _row_stride(d_original), _ptr(d_recovery),
+                                         _row_stride(d_recovery), _stream(stream), ctypes.byref(err)), err)
 
 
 def present_mask(flags) -> bytes:
@@ -627,8 +644,51 @@ def decode_device(original_count: int, recovery_count: int, shard_bytes: int, d_
     op = present_mask(original_present)
     rp = present_mask(recovery_present)
     err = _RsError()
-    _raise(_lib.rs_decode_device(ctx.handle, rate_, original_count, recovery_count, shard_bytes, _ptr(d_original), op,
-                                 _ptr(d_recovery), rp, _ptr(d_restored), _stream(stream), ctypes.byref(err)), err)
+    _raise(_lib.rs_decode_device_strided(ctx.handle, rate_, original_count, recovery_count, shard_bytes,
+                                         _ptr(d_original), _row_stride(d_original), op, _ptr(d_recovery),
+                                         _row_stride(d_recovery), rp, _ptr(d_restored), _row_stride(d_restored),
+                                         _stream(stream), ctypes.byref(err)), err)
+
+
+def _sharded_encode(original_count, recovery_count, shard_bytes, d_original, d_recovery, encode_slice, group=None):
+    """Column-partitioned encode over the ranks of `group`.
+
+    Rank r encodes byte columns [r*w, (r+1)*w), w = shard_bytes / world (whole 64-byte blocks),
+    with encode_slice(orig_cols_view, rec_slice); the [M x w] recovery slices are all-gathered
+    (RCCL over xGMI for the "nccl" backend) and re-interleaved into d_recovery [M x S] on every
+    rank.  Every engine op is column-wise, so the result equals a single-device encode."""
+    import torch
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    if shard_bytes % (64 * world):
+        raise ValueError(f"shard_bytes {shard_bytes} must split into whole 64-byte blocks over {world} ranks")
+    w = shard_bytes // world
+    part = torch.empty((recovery_count, w), dtype=torch.uint8, device=d_recovery.device)
+    encode_slice(d_original[:, rank * w:(rank + 1) * w], part)
+    if dist.get_backend(group) == "nccl":
+        gathered = torch.empty((world, recovery_count, w), dtype=torch.uint8, device=d_recovery.device)
+        dist.all_gather_into_tensor(gathered, part, group=group)
+    else:
+        pieces = [torch.empty_like(part) for _ in range(world)]
+        dist.all_gather(pieces, part, group=group)
+        gathered = torch.stack(pieces)
+    d_recovery.view(recovery_count, world, w).copy_(gathered.permute(1, 0, 2))
+
+
+def encode_device_sharded(original_count: int, recovery_count: int, shard_bytes: int, d_original, d_recovery,
+                          group=None, stream=None, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None) -> None:
+    """Multi-GPU encode of one large stripe: each rank (one GPU each) encodes its column slice of
+    d_original [N x S] on its device, then an all-gather assembles d_recovery [M x S] everywhere."""
+    import torch
+
+    def enc(orig_cols, rec_slice):
+        encode_device(original_count, recovery_count, orig_cols.shape[1], orig_cols, rec_slice,
+                      stream=stream, rate_=rate_, ctx=ctx)
+        if stream is not None:
+            torch.cuda.current_stream().wait_stream(stream)
+
+    _sharded_encode(original_count, recovery_count, shard_bytes, d_original, d_recovery, enc, group)
 
 
 class engine:

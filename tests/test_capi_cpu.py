@@ -196,3 +196,16 @@ def test_work_counts(rs):
         [1, 4096, 5120, 6144, 32768]
     assert [LD.work_count(*x) for x in ((1, 1), (1025, 2048), (1025, 2049), (1024, 3072), (1024, 3073),
                                          (32768, 32768))] == [2, 4096, 8192, 4096, 8192, 65536]
+
+
+def test_python_binding_declares_every_signature():
+    """Every C function the Python mirror calls has ctypes argtypes/restype declared
+    (an undeclared one silently truncates 64-bit pointers to int)."""
+    import re
+    import reed_solomon_simd as rs
+    src = open(rs.__file__).read()
+    used = set(re.findall(r"_lib\.(rs_\w+)", src))
+    assert used
+    for name in sorted(used):
+        f = getattr(rs._lib, name)
+        assert f.argtypes is not None, f"{name} has no declared argtypes"

@@ -494,3 +494,36 @@ def test_chain_repeated_launches_stay_in_sync(torch, rs):
         rs.encode_device(N, M, S, d_orig, d_rec, rate_=1)
     rs.check_device()
     assert np.array_equal(d_rec.cpu().numpy(), want)
+
+
+# ---------------------------------------------------------------------------
+# column-slice (strided) device API: the multi-GPU column partition's building block
+
+@pytest.mark.parametrize("rate,N,M,S,cols", [("high", 1024, 1024, 4096, (1024, 2048)), ("low", 200, 900, 1024, (0, 512)),
+                                             ("high", 5000, 300, 640, (576, 640))])
+def test_strided_column_slice_encode_decode(torch, rs, rate, N, M, S, cols):
+    a, b = cols
+    orig = O.generate_original(N, S, 3)
+    want = O.encode(rate, orig, M)
+    d_orig = _dev(torch, orig)
+    d_rec = torch.full((M, S), 0x77, dtype=torch.uint8, device="cuda")
+    rs.encode_device(N, M, b - a, d_orig[:, a:b], d_rec[:, a:b], rate_=RATE[rate])
+    torch.cuda.synchronize()
+    got = d_rec.cpu().numpy()
+    assert np.array_equal(got[:, a:b], want[:, a:b])
+    assert np.all(got[:, :a] == 0x77) and np.all(got[:, b:] == 0x77), "columns outside the slice untouched"
+    rng = np.random.default_rng(1)
+    L = min(N, M) // 2
+    op = np.ones(N, np.uint8)
+    op[rng.choice(N, L, replace=False)] = 0
+    rp = np.zeros(M, np.uint8)
+    rp[rng.choice(M, L, replace=False)] = 1
+    d_o = _dev(torch, np.where(op[:, None] == 1, orig, 0).astype(np.uint8))
+    d_r = _dev(torch, want)
+    d_out = torch.full((N, S), 0x33, dtype=torch.uint8, device="cuda")
+    rs.decode_device(N, M, b - a, d_o[:, a:b], op, d_r[:, a:b], rp, d_out[:, a:b], rate_=RATE[rate])
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    miss = op == 0
+    assert np.array_equal(out[miss][:, a:b], orig[miss][:, a:b])
+    assert np.all(out[:, :a] == 0x33) and np.all(out[:, b:] == 0x33)
