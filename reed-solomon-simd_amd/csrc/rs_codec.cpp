@@ -271,8 +271,10 @@ bool run_chain(rs_context *ctx, int mode, const Levels &lv, const rs::PassArgs P
     for (int spl = 4; spl <= 6; ++spl) {
         const uint32_t slices = (P[0].packs + (1u << spl) - 1) >> spl;
         if (slices > kChainMaxSlices) continue;
-        const int gb = std::min<int>(int(K1) - 1, 10 - spl);
-        const uint32_t members = std::min<uint32_t>(most, std::max<uint32_t>(1, kChainMaxGroups / slices));
+        const int gb = rs::chain_gb(int(K1), spl);
+        // one block per workgroup and phase (the chain stages all tables up front)
+        const uint32_t members = most;
+        if (uint64_t(slices) * members > kChainMaxGroups) continue;
         if ((uint64_t(slices) * members << (gb + spl)) > kChainMaxThreads) continue;
         rs::ChainArgs C;
         for (int k = 0; k < 3; ++k) {

@@ -75,6 +75,21 @@ hipError_t launch_pass(int K, int flags, const PassArgs &args, hipStream_t strea
 // slice 2^spl); the grid is slices x members workgroups and member q runs
 // blocks q, q + members, ... of each phase's items (set + chunk * nsets).
 enum ChainMode { kChainEncodeHigh = 0, kChainEncodeLow = 1, kChainDecode = 2 };
+// Rows per lane (log2) in the chain's smaller level; workgroups are
+// 2^(K1 - kChainLR) row groups x 2^spl packs (at most 1024 threads).
+#ifndef RS_CHAIN_LR
+#define RS_CHAIN_LR 1
+#endif
+constexpr int kChainLR = RS_CHAIN_LR;
+// log2 row groups of a chain workgroup: at least one wave (2^(gb+spl) >= 64),
+// at most 1024 threads, at least one row per lane in the smaller level.
+constexpr int chain_gb(int K1, int spl) {
+    int gb = K1 - kChainLR;
+    if (gb < 6 - spl) gb = 6 - spl;
+    if (gb > 10 - spl) gb = 10 - spl;
+    if (gb > K1 - 1) gb = K1 - 1;
+    return gb;
+}
 struct ChainArgs {
     PassArgs ph[3];
     uint32_t items[3] = {0, 0, 0};

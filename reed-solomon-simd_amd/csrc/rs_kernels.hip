@@ -194,80 +194,110 @@ __device__ __forceinline__ uint32_t tw_slot(int b, uint32_t j) {
     return (1u << K) - (1u << (K - b)) + (j >> (b + 1));
 }
 
-// Word t of the set's twiddle tables of a transform with skew offset delta.
+// 16-byte piece t (of 5 per table) of the set's twiddle tables of a
+// transform with skew offset delta.
 template <int K>
-__device__ __forceinline__ uint32_t twiddle_word(const PassArgs &A, const Ctx &c, uint32_t delta, uint32_t t) {
-    const uint32_t slot = t / 20, word = t - slot * 20;
+__device__ __forceinline__ uint4 twiddle_piece(const PassArgs &A, const Ctx &c, uint32_t delta, uint32_t t) {
+    const uint32_t slot = t / 5, piece = t - slot * 5;
     const uint32_t y = (1u << K) - slot;            // in [2, 2^K]
     const int b = K - (32 - __builtin_clz(y - 1));  // K - ceil(log2 y)
     const uint32_t grp = slot - ((1u << K) - (1u << (K - b)));
     const uint32_t row = c.grow(grp << (b + 1), K);
     const uint32_t gb = c.a + b;
     const uint32_t idx = (row & ~((2u << gb) - 1u)) + (1u << gb) + delta - 1u;
-    return A.tw[idx * 20u + word];
+    return reinterpret_cast<const uint4 *>(A.tw)[idx * 5u + piece];
 }
 
-// Stage tables into LDS (null destinations are skipped).  No barrier.  NT =
-// workgroup size: each thread issues all its global loads before its LDS
-// stores, so staging costs one memory round trip (two for decode tables,
-// whose address depends on the row's log factor).
+// Staging of a block's tables into LDS (null destinations are skipped), in
+// two halves so several blocks' staging can share one memory round trip:
+// load() issues every global load into registers, store() writes LDS.  NT =
+// workgroup size.  Twiddles: one round trip; decode row tables: two (their
+// address depends on the row's log factor).  No barrier.
 template <int K, int NT>
-__device__ __forceinline__ void stage(const PassArgs &A, const Ctx &c, uint32_t chunk, uint32_t *tabI, uint32_t dI,
-                                      uint32_t *tabF, uint32_t dF, uint32_t *tabS, uint32_t *tabV,
-                                      uint32_t *rinfo) {
-    constexpr uint32_t kTw = ((1u << K) - 1) * 20, kRw = 20u << K;
-    constexpr int PT = kTw ? (kTw + NT - 1) / NT : 1, PR = (kRw + NT - 1) / NT;
-    const uint32_t tid = threadIdx.x;
+struct Stager {
+    // in 16-byte pieces: 5 per 20-word table
+    static constexpr uint32_t kTw = ((1u << K) - 1) * 5, kRw = 5u << K;
+    static constexpr int PT = kTw ? (kTw + NT - 1) / NT : 1, PR = (kRw + NT - 1) / NT;
+    uint32_t *tabI = nullptr, *tabF = nullptr, *tabS = nullptr, *tabV = nullptr, *rinfo = nullptr;
+    uint4 vi[PT], vf[PT], vs[PR], vv[PR];
+    uint32_t ri = 0;
+
+    __device__ __forceinline__ void load(const PassArgs &A, const Ctx &c, uint32_t chunk) {
 #ifdef RS_PROBE_SKIP_STAGE  // tools/pass_probe.hip: time a pass without table staging
-    return;
+        return;
 #endif
-    uint32_t vi[PT], vf[PT];
-    if (tabI || tabF) {
+        const uint32_t tid = threadIdx.x;
+        const uint32_t dI = A.ifft_delta + chunk * A.ifft_delta_step, dF = A.fft_delta + chunk * A.fft_delta_step;
+        if (tabI || tabF) {
 #pragma unroll
-        for (int k = 0; k < PT; ++k) {
-            const uint32_t t = tid + uint32_t(k) * NT;
-            if (t < kTw) {
-                if (tabI) vi[k] = twiddle_word<K>(A, c, dI, t);
-                if (tabF) vf[k] = twiddle_word<K>(A, c, dF, t);
+            for (int k = 0; k < PT; ++k) {
+                const uint32_t t = tid + uint32_t(k) * NT;
+                if (t < kTw) {
+                    if (tabI) vi[k] = twiddle_piece<K>(A, c, dI, t);
+                    if (tabF) vf[k] = twiddle_piece<K>(A, c, dF, t);
+                }
+            }
+        }
+        if (tabS || tabV) {
+            uint32_t f[PR];
+#pragma unroll
+            for (int k = 0; k < PR; ++k) {
+                const uint32_t t = tid + uint32_t(k) * NT;
+                if (t < kRw) f[k] = A.rowinfo[c.grow(t / 5, K) + chunk * A.n];
+            }
+            if (tid < (1u << K)) ri = A.rowinfo[c.grow(tid, K) + chunk * A.n];
+            const uint4 *lut4 = reinterpret_cast<const uint4 *>(A.lut);
+#pragma unroll
+            for (int k = 0; k < PR; ++k) {
+                const uint32_t t = tid + uint32_t(k) * NT;
+                if (t < kRw) {
+                    const uint32_t piece = t % 5, lf = f[k] & 0xFFFFu;
+                    if (tabS) vs[k] = lut4[lf * 5u + piece];
+                    if (tabV) vv[k] = lut4[(65535u - lf) * 5u + piece];
+                }
             }
         }
     }
-    if (tabS || tabV) {
-        uint32_t f[PR], vs[PR], vv[PR];
+
+    __device__ __forceinline__ void store() const {
+#ifdef RS_PROBE_SKIP_STAGE
+        return;
+#endif
+        const uint32_t tid = threadIdx.x;
+        if (tabI || tabF) {
 #pragma unroll
-        for (int k = 0; k < PR; ++k) {
-            const uint32_t t = tid + uint32_t(k) * NT;
-            if (t < kRw) f[k] = A.rowinfo[c.grow(t / 20, K) + chunk * A.n];
-        }
-        if (tid < (1u << K)) rinfo[tid] = A.rowinfo[c.grow(tid, K) + chunk * A.n];
-#pragma unroll
-        for (int k = 0; k < PR; ++k) {
-            const uint32_t t = tid + uint32_t(k) * NT;
-            if (t < kRw) {
-                const uint32_t word = t % 20, lf = f[k] & 0xFFFFu;
-                if (tabS) vs[k] = A.lut[lf * 20u + word];
-                if (tabV) vv[k] = A.lut[(65535u - lf) * 20u + word];
+            for (int k = 0; k < PT; ++k) {
+                const uint32_t t = tid + uint32_t(k) * NT;
+                if (t < kTw) {
+                    if (tabI) reinterpret_cast<uint4 *>(tabI)[t] = vi[k];
+                    if (tabF) reinterpret_cast<uint4 *>(tabF)[t] = vf[k];
+                }
             }
         }
+        if (tabS || tabV) {
+            if (tid < (1u << K)) rinfo[tid] = ri;
 #pragma unroll
-        for (int k = 0; k < PR; ++k) {
-            const uint32_t t = tid + uint32_t(k) * NT;
-            if (t < kRw) {
-                if (tabS) tabS[t] = vs[k];
-                if (tabV) tabV[t] = vv[k];
-            }
-        }
-    }
-    if (tabI || tabF) {
-#pragma unroll
-        for (int k = 0; k < PT; ++k) {
-            const uint32_t t = tid + uint32_t(k) * NT;
-            if (t < kTw) {
-                if (tabI) tabI[t] = vi[k];
-                if (tabF) tabF[t] = vf[k];
+            for (int k = 0; k < PR; ++k) {
+                const uint32_t t = tid + uint32_t(k) * NT;
+                if (t < kRw) {
+                    if (tabS) reinterpret_cast<uint4 *>(tabS)[t] = vs[k];
+                    if (tabV) reinterpret_cast<uint4 *>(tabV)[t] = vv[k];
+                }
             }
         }
     }
+};
+
+// Only the IFFT (or only the FFT) tables of one chunk: the per-chunk
+// re-staging of multi-chunk passes.
+template <int K, int NT>
+__device__ __forceinline__ void stage_twiddles(const PassArgs &A, const Ctx &c, uint32_t chunk, uint32_t *tabI,
+                                               uint32_t *tabF) {
+    Stager<K, NT> st;
+    st.tabI = tabI;
+    st.tabF = tabF;
+    st.load(A, c, chunk);
+    st.store();
 }
 
 // Load the lane's rows (phase PH) of `chunk`.  SCALE: rows erased in the
@@ -531,11 +561,53 @@ __device__ __forceinline__ void transform(const Ctx &c, uint32_t *plane, const u
     }
 }
 
+template <int K, int LR, int SPL>
+__device__ __forceinline__ Ctx make_ctx(const PassArgs &A, uint32_t bx) {
+    using P = Pass<K, LR, SPL>;
+    Ctx c;
+    c.p = threadIdx.x & (P::SP - 1);
+    c.g = threadIdx.x >> SPL;
+    if constexpr (P::kUniform) c.g = __builtin_amdgcn_readfirstlane(c.g);
+    const uint32_t slice = bx % A.slices;
+    const uint32_t set = bx / A.slices;
+    c.a = A.a;
+    c.s_lo = set & ((1u << A.a) - 1u);
+    c.s_hi = set >> A.a;
+    const uint32_t pk = slice * P::SP + c.p;
+    c.pk_ok = pk < A.packs;
+    c.pk_off = (pk >> 3) * 64u + (pk & 7u) * 4u;
+    return c;
+}
+
+// The stager of the tables a pass block needs, targeting its LDS layout.
+template <int K, int LR, int SPL, int FLAGS>
+__device__ __forceinline__ Stager<K, Pass<K, LR, SPL>::kThreads> stager_for(uint32_t *lds) {
+    using L = Lds<K, SPL, FLAGS>;
+    constexpr bool DO_IFFT = FLAGS & kIfft, DO_FFT = FLAGS & kFft, MULTI_OUT = FLAGS & kMultiOut;
+    constexpr bool SCALE = FLAGS & kScale, REVEAL = FLAGS & kReveal;
+    Stager<K, Pass<K, LR, SPL>::kThreads> st;
+    if constexpr (K > 0 && DO_IFFT) st.tabI = lds + L::oI;
+    if constexpr (K > 0 && DO_FFT && !MULTI_OUT) st.tabF = lds + L::oF;
+    if constexpr (SCALE) st.tabS = lds + L::oS;
+    if constexpr (REVEAL) st.tabV = lds + L::oV;
+    if constexpr (SCALE || REVEAL) st.rinfo = lds + L::oR;
+    return st;
+}
+
+struct NoExtra {
+    __device__ __forceinline__ void operator()() const {}
+};
+
 // One pass over workgroup-block (bx = set * slices + slice, by = chunk).
 // COH_LD / COH_ST: work-buffer rows are handed between workgroups of one
 // launch (k_chain phases), so they are read / written coherently.
-template <int K, int LR, int SPL, int FLAGS, bool COH_LD, bool COH_ST, int STAMP = -1>
-__device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32_t by, uint32_t *lds) {
+// STAGED: the block's tables are staged by the caller, whose `extra` runs
+// between the row loads and the barrier (k_chain stages every phase's tables
+// in phase 0's load window).
+template <int K, int LR, int SPL, int FLAGS, bool COH_LD, bool COH_ST, int STAMP = -1, bool STAGED = false,
+          typename Extra = NoExtra>
+__device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32_t by, uint32_t *lds,
+                                          const Extra &extra = Extra()) {
     using P = Pass<K, LR, SPL>;
     using L = Lds<K, SPL, FLAGS>;
     constexpr bool DO_IFFT = FLAGS & kIfft;
@@ -552,31 +624,21 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
     uint32_t *tabI = lds + L::oI, *tabF = lds + L::oF, *tabS = lds + L::oS, *tabV = lds + L::oV;
     uint32_t *rinfo = lds + L::oR;
 
-    Ctx c;
-    c.p = threadIdx.x & (P::SP - 1);
-    c.g = threadIdx.x >> SPL;
-    if constexpr (P::kUniform) c.g = __builtin_amdgcn_readfirstlane(c.g);
-    const uint32_t slice = bx % A.slices;
-    const uint32_t set = bx / A.slices;
+    const Ctx c = make_ctx<K, LR, SPL>(A, bx);
     const uint32_t gchunk = by;
-    c.a = A.a;
-    c.s_lo = set & ((1u << A.a) - 1u);
-    c.s_hi = set >> A.a;
-    const uint32_t pk = slice * P::SP + c.p;
-    c.pk_ok = pk < A.packs;
-    c.pk_off = (pk >> 3) * 64u + (pk & 7u) * 4u;
 
     uint32_t lo[P::R], hi[P::R];
     uint32_t xl[XOR_IN ? P::R : 1], xh[XOR_IN ? P::R : 1];
     // loads first, then table staging: one barrier covers both latencies
     load_rows<K, LR, SPL, DO_IFFT ? 0 : PL, SCALE, COH_LD>(A, c, gchunk, lo, hi);
     if constexpr (XOR_IN) load_xor_rows<K, LR, SPL, PL, COH_LD>(A, c, xl, xh);
-    if constexpr (K > 0)
-        stage<K, P::kThreads>(A, c, gchunk, DO_IFFT ? tabI : nullptr, A.ifft_delta + gchunk * A.ifft_delta_step,
-                 DO_FFT && !MULTI_OUT ? tabF : nullptr, A.fft_delta + gchunk * A.fft_delta_step,
-                 SCALE ? tabS : nullptr, REVEAL ? tabV : nullptr, rinfo);
-    else
-        stage<K, P::kThreads>(A, c, gchunk, nullptr, 0, nullptr, 0, SCALE ? tabS : nullptr, REVEAL ? tabV : nullptr, rinfo);
+    if constexpr (!STAGED) {
+        auto st = stager_for<K, LR, SPL, FLAGS>(lds);
+        st.load(A, c, gchunk);
+        st.store();
+    } else {
+        extra();
+    }
     __syncthreads();
     if constexpr (STAMP >= 0) RS_STAMP(STAMP);
     if constexpr (SCALE) scale_rows<K, LR, SPL, 0>(c, tabS, lo, hi);
@@ -589,9 +651,7 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
                 uint32_t tl[P::R], th[P::R];
                 load_rows<K, LR, SPL, 0, false, COH_LD>(A, c, chunk, tl, th);
                 __syncthreads();
-                if constexpr (K > 0)
-                    stage<K, P::kThreads>(A, c, chunk, tabI, A.ifft_delta + chunk * A.ifft_delta_step, nullptr, 0, nullptr, nullptr,
-                             nullptr);
+                if constexpr (K > 0) stage_twiddles<K, P::kThreads>(A, c, chunk, tabI, nullptr);
                 __syncthreads();
                 transform<K, LR, SPL, true>(c, plane, tabI, tl, th);
                 static_for<0, P::R>([&](auto ic) { lo[ic] ^= tl[ic]; hi[ic] ^= th[ic]; });
@@ -613,9 +673,7 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
             uint32_t yl[P::R], yh[P::R];
             static_for<0, P::R>([&](auto ic) { yl[ic] = lo[ic]; yh[ic] = hi[ic]; });
             __syncthreads();
-            if constexpr (K > 0)
-                stage<K, P::kThreads>(A, c, chunk, nullptr, 0, tabF, A.fft_delta + chunk * A.fft_delta_step, nullptr, nullptr,
-                         nullptr);
+            if constexpr (K > 0) stage_twiddles<K, P::kThreads>(A, c, chunk, nullptr, tabF);
             __syncthreads();
             transform<K, LR, SPL, false>(c, plane, tabF, yl, yh);
             store_rows<K, LR, SPL, 0, false, COH_ST>(A, c, chunk, tabV, rinfo, yl, yh);
@@ -705,11 +763,16 @@ hipError_t launch_shape(bool narrow, int flags, const PassArgs &A, hipStream_t s
 // bounded (a timed-out wait sets *fault instead of hanging the device).
 constexpr uint32_t kSpinLimit = 1u << 21;
 
-__device__ __forceinline__ void slice_barrier(uint32_t *ctr, uint32_t members, uint32_t *fault) {
+// `during` runs on every thread between this workgroup's arrival and the
+// wait (loads issued there overlap the barrier).
+template <typename During = NoExtra>
+__device__ __forceinline__ void slice_barrier(uint32_t *ctr, uint32_t members, uint32_t *fault,
+                                              const During &during = During()) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    during();
     if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t spins = 0;
         while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < members) {
             __builtin_amdgcn_s_sleep(1);
@@ -720,13 +783,6 @@ __device__ __forceinline__ void slice_barrier(uint32_t *ctr, uint32_t members, u
         }
     }
     __syncthreads();
-}
-
-// Row-group bits of a chain workgroup: equal in both levels (the block size
-// is fixed), LR = K - GB rows per lane.
-template <int K1, int SPL>
-constexpr int chain_gb() {
-    return K1 - 1 < 10 - SPL ? K1 - 1 : 10 - SPL;
 }
 
 template <int MODE>
@@ -744,34 +800,61 @@ struct ChainFlags<kChainDecode> {
     static constexpr int F0 = kIfft | kScale, F1 = kIfft | kFft | kFd, F2 = kFft | kFd | kXorIn | kReveal;
 };
 
-template <int K, int LR, int SPL, int FLAGS, bool COH_LD, bool COH_ST, int STAMP>
-__device__ __forceinline__ void chain_phase(const ChainArgs &C, const PassArgs &A, uint32_t items, uint32_t slice,
-                                            uint32_t q, uint32_t *lds) {
-    for (uint32_t it = q; it < items; it += C.members) {
-        if (it != q) __syncthreads();  // the previous item's LDS readers are done
-        const uint32_t set = it % A.nsets, chunk = it / A.nsets;
-        pass_body<K, LR, SPL, FLAGS, COH_LD, COH_ST, STAMP>(A, set * A.slices + slice, chunk, lds);
-    }
+// LDS words of a phase region (16-byte aligned)
+template <int K, int SPL, int FLAGS>
+constexpr uint32_t chain_region() {
+    return (Lds<K, SPL, FLAGS>::words + 3u) & ~3u;
 }
 
 template <int K0, int K1, int SPL, int MODE>
-__global__ void __launch_bounds__(1 << (chain_gb<K1, SPL>() + SPL)) k_chain(const ChainArgs C) {
+__global__ void __launch_bounds__(1 << (chain_gb(K1, SPL) + SPL)) k_chain(const ChainArgs C) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    constexpr int GB = chain_gb<K1, SPL>();
+    constexpr int GB = chain_gb(K1, SPL);
+    constexpr int LR0 = K0 - GB, LR1 = K1 - GB;
     using Fl = ChainFlags<MODE>;
+    // every phase's tables stay resident: one staging round trip for all three
+    uint32_t *lds0 = lds;
+    uint32_t *lds1 = lds0 + chain_region<K0, SPL, Fl::F0>();
+    uint32_t *lds2 = lds1 + chain_region<K1, SPL, Fl::F1>();
     const uint32_t nsl = C.ph[0].slices;
     const uint32_t slice = blockIdx.x % nsl, q = blockIdx.x / nsl;
     uint32_t *ctr = C.sync + slice * 32u;
     RS_STAMP(0);
-    chain_phase<K0, K0 - GB, SPL, Fl::F0, false, true, 8>(C, C.ph[0], C.items[0], slice, q, lds);
+    // Workgroup q runs item q of each phase (the host guarantees items[p] <=
+    // members): set q % nsets, chunk q / nsets.
+    uint32_t bx[3], by[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        bx[p] = (q % C.ph[p].nsets) * nsl + slice;
+        by[p] = q / C.ph[p].nsets;
+    }
+    // Table staging off the critical path: phase 0's tables load beside its
+    // row loads; phase 1's and 2's load while the workgroup waits at the
+    // preceding slice barrier, and land in LDS right after it.
+    const bool a0 = q < C.items[0], a1 = q < C.items[1], a2 = q < C.items[2];
+    auto s0 = stager_for<K0, LR0, SPL, Fl::F0>(lds0);
+    auto s1 = stager_for<K1, LR1, SPL, Fl::F1>(lds1);
+    auto s2 = stager_for<K0, LR0, SPL, Fl::F2>(lds2);
+    if (a0) {
+        pass_body<K0, LR0, SPL, Fl::F0, false, true, 8, true>(C.ph[0], bx[0], by[0], lds0, [&]() {
+            s0.load(C.ph[0], make_ctx<K0, LR0, SPL>(C.ph[0], bx[0]), by[0]);
+            s0.store();
+        });
+    }
     RS_STAMP(1);
-    slice_barrier(ctr, C.members, C.fault);
+    slice_barrier(ctr, C.members, C.fault, [&]() {
+        if (a1) s1.load(C.ph[1], make_ctx<K1, LR1, SPL>(C.ph[1], bx[1]), by[1]);
+    });
+    if (a1) s1.store();
     RS_STAMP(2);
-    chain_phase<K1, K1 - GB, SPL, Fl::F1, true, true, 10>(C, C.ph[1], C.items[1], slice, q, lds);
+    if (a1) pass_body<K1, LR1, SPL, Fl::F1, true, true, 10, true>(C.ph[1], bx[1], by[1], lds1);
     RS_STAMP(3);
-    slice_barrier(ctr + 1, C.members, C.fault);
+    slice_barrier(ctr + 1, C.members, C.fault, [&]() {
+        if (a2) s2.load(C.ph[2], make_ctx<K0, LR0, SPL>(C.ph[2], bx[2]), by[2]);
+    });
+    if (a2) s2.store();
     RS_STAMP(4);
-    chain_phase<K0, K0 - GB, SPL, Fl::F2, true, false, 12>(C, C.ph[2], C.items[2], slice, q, lds);
+    if (a2) pass_body<K0, LR0, SPL, Fl::F2, true, false, 12, true>(C.ph[2], bx[2], by[2], lds2);
     RS_STAMP(5);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     RS_STAMP(6);
@@ -789,11 +872,10 @@ __global__ void __launch_bounds__(1 << (chain_gb<K1, SPL>() + SPL)) k_chain(cons
 
 template <int K0, int K1, int SPL, int MODE>
 hipError_t launch_chain_f(const ChainArgs &C, hipStream_t s) {
-    constexpr int GB = chain_gb<K1, SPL>();
+    constexpr int GB = chain_gb(K1, SPL);
     using Fl = ChainFlags<MODE>;
-    constexpr size_t l0 = Lds<K0, SPL, Fl::F0>::bytes(), l1 = Lds<K1, SPL, Fl::F1>::bytes(),
-                     l2 = Lds<K0, SPL, Fl::F2>::bytes();
-    constexpr size_t lds = l0 > l1 ? (l0 > l2 ? l0 : l2) : (l1 > l2 ? l1 : l2);
+    constexpr size_t lds = size_t(chain_region<K0, SPL, Fl::F0>() + chain_region<K1, SPL, Fl::F1>() +
+                                  chain_region<K0, SPL, Fl::F2>()) * 4;
     static bool attr_set = false;
     if (!attr_set && lds > 65536) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_chain<K0, K1, SPL, MODE>),
