@@ -408,13 +408,42 @@ __device__ __forceinline__ void layer(const Ctx &c, const uint32_t *tab, uint32_
     });
 }
 
-// Move the rows from phase FROM to phase TO through LDS (both planes at once).
+// 2x2 transpose between lane rows 16 (LANE_BIT 4) or 32 (LANE_BIT 5) apart:
+// the lane with lane bit clear keeps a and takes its partner's a as b, the
+// partner keeps b and takes the a-lane's b as a (v_permlane{16,32}_swap).
+template <int LANE_BIT>
+__device__ __forceinline__ void lane_transpose(uint32_t &a, uint32_t &b) {
+    if constexpr (LANE_BIT == 4) {
+        const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+        a = r[0];
+        b = r[1];
+    } else {
+        static_assert(LANE_BIT == 5, "in-wave row-group bits are lane bits 4 and 5");
+        const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+        a = r[0];
+        b = r[1];
+    }
+}
+
+// Move the rows from phase FROM to phase TO: through LDS (both planes at
+// once), or -- 2 rows per lane, adjacent phases whose differing row-group bit
+// lies inside the wave -- by a cross-lane transpose without LDS or barrier.
 template <int K, int LR, int SPL, int FROM, int TO>
 __device__ __forceinline__ void exchange(const Ctx &c, uint32_t *plane, uint32_t (&lo)[1 << LR],
                                          uint32_t (&hi)[1 << LR]) {
     using P = Pass<K, LR, SPL>;
     constexpr uint32_t kPlane = uint32_t(P::SP) << K;
     if constexpr (FROM == TO) return;
+    if constexpr (LR == 1 && (TO == FROM + 1 || FROM == TO + 1)) {
+        // phases p and p+1 hold register bit p resp. p+1; the rows of lanes whose
+        // row groups differ only in group bit p (row bit p+1 / p) are transposed
+        constexpr int p = FROM < TO ? FROM : TO;
+        if constexpr (SPL + p == 4 || SPL + p == 5) {
+            lane_transpose<SPL + p>(lo[0], lo[1]);
+            lane_transpose<SPL + p>(hi[0], hi[1]);
+            return;
+        }
+    }
     __syncthreads();
     static_for<0, P::R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
@@ -737,13 +766,14 @@ hipError_t launch_k(int flags, const PassArgs &A, hipStream_t s) {
 }
 
 // Two shapes per K: "wide" (64-pack slices, 8 rows per lane) for matrices
-// that fill the chip, "narrow" (16..32-pack slices, 2..4 rows per lane) to
-// spread small matrices over more workgroups and waves.
+// that fill the chip, "narrow" (16..32-pack slices, 2 rows per lane, in-wave
+// phase changes by lane transposes) to spread small matrices over more
+// workgroups and waves.
 template <int K>
 hipError_t launch_shape(bool narrow, int flags, const PassArgs &A, hipStream_t s) {
     constexpr int LRW = K < 3 ? K : 3;
     if constexpr (K >= 2) {
-        constexpr int LRN = K < 3 ? 1 : 2;
+        constexpr int LRN = 1;
         constexpr int SPLN = 6 - (K - LRN) > 4 ? 6 - (K - LRN) : 4;
         if (narrow) return launch_k<K, LRN, SPLN>(flags, A, s);
     }
