@@ -136,15 +136,28 @@ def main():
         a[0] += ms
         a[1] += 1
         a[2] += by
-    kernels = {k: {"launches_per_step": v[1] / args.profile_steps, "avg_us": 1e3 * v[0] / v[1],
-                   "bytes_per_launch": v[2] // v[1]} for k, v in agg.items()}
+    kernels = {k: {"launches_per_step": v[1] / args.profile_steps, "avg_us": round(1e3 * v[0] / v[1], 3),
+                   "rows_bytes_per_launch": v[2] // v[1]} for k, v in agg.items()}
     dom = max(agg, key=lambda k: agg[k][0])
     dom_avg_s = agg[dom][0] / agg[dom][1] / 1e3
-    achieved = kernels[dom]["bytes_per_launch"] / dom_avg_s / 1e9
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "bytes_per_launch": kernels[dom]["bytes_per_launch"], "avg_us": round(dom_avg_s * 1e6, 3),
-                "kernels": kernels}
+    # Algorithmic bytes: an encode must read N*S original
+    # bytes and write M*S recovery bytes.  When one launch does the whole
+    # encode (the headline's chain kernel) that is its per-launch figure;
+    # otherwise the step's algorithmic bytes are priced against the summed
+    # duration of all the step's launches.
+    alg_step = (N + M) * S
+    kernel_s_per_step = sum(v[0] for v in agg.values()) / 1e3 / args.profile_steps
+    if len(agg) == 1 and kernels[dom]["launches_per_step"] == 1:
+        scope, achieved = "launch", alg_step / dom_avg_s / 1e9
+    else:
+        scope, achieved = "step (all launches)", alg_step / kernel_s_per_step / 1e9
+    traffic = load_traffic(dom)
+    roofline = {"bound": "hbm", "kernel": dom, "scope": scope, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": traffic["hbm_bytes"] if traffic else None,
+                "traffic_source": traffic["source"] if traffic else None,
+                "algorithmic_bytes": alg_step,
+                "avg_us": round(dom_avg_s * 1e6, 3), "kernels": kernels}
 
     # ---- decode at 1 % and 100 % loss (benchmarks.rs:113-138) --------------
     decode = {}
@@ -182,6 +195,23 @@ def main():
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def load_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/<tag>/traffic.json, written by tools/pmc_traffic.py from
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same bench)."""
+    pdir = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(pdir):
+        return None
+    for tag in sorted(os.listdir(pdir), reverse=True):
+        f = os.path.join(pdir, tag, "traffic.json")
+        if os.path.exists(f):
+            with open(f) as fh:
+                d = json.load(fh)
+            if kernel in d["kernels"]:
+                return {"hbm_bytes": d["kernels"][kernel]["hbm_bytes"], "source": f"profiles/{tag}/traffic.json"}
+    return None
 
 
 def cpu_baseline(seconds):

@@ -293,9 +293,9 @@ bool run_chain(rs_context *ctx, int mode, const Levels &lv, const rs::PassArgs P
         if (e == hipErrorNotSupported) return false;
         check(e);
         if (t_prof_ctx) {
-            static const char *names[3] = {"k_chain_encode_high", "k_chain_encode_low", "k_chain_decode"};
+            // same spelling as the rocprofv3 kernel trace (template arguments)
             static thread_local char buf[64];
-            snprintf(buf, sizeof buf, "%s<K=%u+%u>", names[mode], K0, K1);
+            snprintf(buf, sizeof buf, "k_chain<%u, %u, %d, %d>", K0, K1, spl, mode);
             // algorithmic bytes: the three passes' reads + writes
             uint64_t bytes = 0;
             for (int k = 0; k < 3; ++k)
