@@ -210,6 +210,16 @@ int rs_profile_collect(rs_context *ctx, float *ms, uint64_t *bytes, const char *
 rs_status rs_chain_enable(rs_context *ctx, int enable);
 rs_status rs_check_device(rs_context *ctx);
 
+/* ---- column kernel control (engine tuning, not a reference item) ----
+ * Transforms of 2^7 .. 2^12 rows over at most RS_MI355X_MONO_MAX_PACKS (4096)
+ * packs of 4 elements run as one launch in which a workgroup owns every row
+ * of one pack (DESIGN.md "Column kernel").  rs_mono_enable(ctx, 0) selects
+ * the pass / chain kernels instead (also: RS_MI355X_NO_MONO=1 at context
+ * creation); 1 (default) uses it where it is fastest (single-chunk transforms
+ * of 2^7 .. 2^10 rows, twiddles staged in LDS); 2 also for multi-chunk and
+ * 2^11 / 2^12-row transforms (also: RS_MI355X_MONO_ALL=1). */
+rs_status rs_mono_enable(rs_context *ctx, int enable);
+
 /* ---- GF(2^16) tables (src/engine/tables.rs), host copies ---- */
 const uint16_t *rs_table_exp(void);       /* 65536 */
 const uint16_t *rs_table_log(void);       /* 65536 */

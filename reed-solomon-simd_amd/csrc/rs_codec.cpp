@@ -128,6 +128,11 @@ struct rs_context {
     uint32_t *d_sync = nullptr;   // chain-kernel barrier counters (kChainMaxSlices x 32 words)
     uint32_t *d_fault = nullptr;  // set by a chain kernel whose barrier wait gave up
     bool chain = true;            // RS_MI355X_NO_CHAIN=1 disables the chain kernel
+    bool mono = true;             // RS_MI355X_NO_MONO=1 disables the column kernel
+    bool mono_all = false;        // RS_MI355X_MONO_ALL=1: unstaged column kernel too (see use_mono)
+    uint32_t mono_max_packs = 4096;  // column kernel only up to this many packs (RS_MI355X_MONO_MAX_PACKS)
+    std::mutex img_mu;            // guards d_img
+    uint32_t *d_img[13] = {};     // column-kernel twiddle images per L (built on first use)
     std::mutex mu;  // guards ws (device-resident API scratch)
     Workspace ws;
     // kernel timing (rs_profile_enable)
@@ -307,6 +312,64 @@ bool run_chain(rs_context *ctx, int mode, const Levels &lv, const rs::PassArgs P
     return false;
 }
 
+// Column kernel (rs_mono.hip): twiddle images of a 2^L-row transform for
+// every skew offset t * n, t = 0 .. 65536/n - 1 (rs_device.hpp), built on the
+// host from the skew tables once per context and L.
+constexpr uint32_t kMonoMinL = 7, kMonoMaxL = 12;
+const uint32_t *mono_images(rs_context *ctx, uint32_t L) {
+    std::lock_guard<std::mutex> lock(ctx->img_mu);
+    if (ctx->d_img[L]) return ctx->d_img[L];
+    const rs::GfTables &T = rs::tables();
+    const uint32_t n = 1u << L, nimg = 65536u / n;  // skew offsets t * n + (n - 2) <= 65534
+    const size_t words = size_t(n - 1) * rs::kPermWords;
+    std::vector<uint32_t> h(words * nimg);
+    for (uint32_t t = 0; t < nimg; ++t) {
+        uint32_t *dst = &h[t * words];
+        for (uint32_t b = 0; b < L; ++b)
+            for (uint32_t g = 0; g < (n >> (b + 1)); ++g) {
+                const uint32_t slot = n - (n >> b) + g;
+                const uint32_t idx = (g << (b + 1)) + (1u << b) + t * n - 1;
+                std::copy_n(&T.perm_by_skew[size_t(idx) * rs::kPermWords], rs::kPermWords,
+                            dst + size_t(slot) * rs::kPermWords);
+            }
+    }
+    uint32_t *d = nullptr;
+    check(hipMalloc(&d, h.size() * 4));
+    check(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    ctx->d_img[L] = d;
+    return d;
+}
+
+// The column kernel runs where it beats the pass / chain kernels: its staged
+// variant (one chunk, L <= 10).  RS_MI355X_MONO_ALL=1 also routes multi-chunk
+// and L = 11, 12 transforms to its unstaged variant (tests, tuning).
+bool use_mono(rs_context *ctx, uint32_t L, const Geom &g, uint32_t chunks) {
+    if (!ctx->mono || L < kMonoMinL || L > kMonoMaxL || g.packs > ctx->mono_max_packs) return false;
+    return ctx->mono_all || rs::mono_staged(int(L), chunks);
+}
+
+rs::MonoArgs mono_args(rs_context *ctx, uint32_t L, const Geom &g) {
+    rs::MonoArgs M;
+    M.packs = g.packs;
+    M.packs_per_xcd = (g.packs + 7) / 8;
+    M.img = mono_images(ctx, L);
+    M.img_words = uint64_t((1u << L) - 1) * rs::kPermWords;
+    M.lut = ctx->d_lut;
+    return M;
+}
+
+void launch_mono(int mode, uint32_t L, const rs::MonoArgs &M, hipStream_t s, uint64_t bytes) {
+    hipEvent_t ev = nullptr;
+    if (t_prof_ctx) prof_begin(s, &ev);
+    check(rs::launch_mono(mode, int(L), M, s));
+    if (t_prof_ctx) {
+        static thread_local char buf[64];
+        snprintf(buf, sizeof buf, "k_mono<%u, %d, %d, %s>", L, rs::mono_rows_log2_per_lane(int(L)), mode,
+                 rs::mono_staged(int(L), M.chunks) ? "true" : "false");
+        prof_end(s, ev, buf, bytes);
+    }
+}
+
 // HighRate encode (rate_high.rs:44-87) from device rows to device rows:
 // chunk c's IFFT uses skew_delta c*n + n, the chunks are XOR-folded, one FFT
 // with skew_delta 0 produces the recovery rows.
@@ -319,6 +382,18 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
     A.ifft_delta = n;
     A.ifft_delta_step = n;
     const rs::RowMap src{orig, g.orig(), 0, uint32_t(N)}, dst{rec, g.rec(), 0, uint32_t(M)};
+    if (use_mono(ctx, L, g, C)) {
+        rs::MonoArgs Mo = mono_args(ctx, L, g);
+        Mo.src[0] = src;
+        Mo.nsrc = 1;
+        Mo.dst = dst;
+        Mo.chunks = C;
+        Mo.ifft_img = 1;  // chunk c: skew offset c * n + n
+        Mo.ifft_img_step = 1;
+        Mo.fft_img = 0;
+        launch_mono(rs::kMonoEncodeHigh, L, Mo, s, (N + M) * uint64_t(g.packs) * 8);
+        return;
+    }
     if (lv.m == 1) {
         A.src[0] = src;
         A.nsrc = 1;
@@ -369,6 +444,18 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
     A.fft_delta = n;
     A.fft_delta_step = n;
     const rs::RowMap src{orig, g.orig(), 0, uint32_t(N)}, dst{rec, g.rec(), 0, uint32_t(M)};
+    if (use_mono(ctx, L, g, C)) {
+        rs::MonoArgs Mo = mono_args(ctx, L, g);
+        Mo.src[0] = src;
+        Mo.nsrc = 1;
+        Mo.dst = dst;
+        Mo.chunks = C;
+        Mo.ifft_img = 0;
+        Mo.fft_img = 1;  // output chunk c: skew offset c * n + n
+        Mo.fft_img_step = 1;
+        launch_mono(rs::kMonoEncodeLow, L, Mo, s, (N + M) * uint64_t(g.packs) * 8);
+        return;
+    }
     if (lv.m == 1) {
         A.src[0] = src;
         A.nsrc = 1;
@@ -449,6 +536,16 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
     const rs::RowMap rec_map{rec, g.rec(), high ? 0u : chunk, high ? uint32_t(M) : end};
     const rs::RowMap orig_map{orig, g.orig(), high ? chunk : 0u, high ? end : uint32_t(N)};
     const rs::RowMap out_map{restored, g.out(), orig_map.row_begin, orig_map.row_end};
+    if (use_mono(ctx, u, g, 1)) {
+        rs::MonoArgs Mo = mono_args(ctx, u, g);
+        Mo.src[0] = rec_map;
+        Mo.src[1] = orig_map;
+        Mo.nsrc = 2;
+        Mo.dst = out_map;
+        Mo.rowinfo = d_rowinfo;
+        launch_mono(rs::kMonoDecode, u, Mo, s, (received + missing) * uint64_t(g.packs) * 8);
+        return;
+    }
     const Levels lv = levels(u);
     if (lv.m == 1) {
         A.src[0] = rec_map;
@@ -642,6 +739,11 @@ rs_status rs_context_create(int device, rs_context **out) {
         check(hipMemset(ctx->d_fault, 0, 4));
         const char *nc = getenv("RS_MI355X_NO_CHAIN");
         ctx->chain = !(nc && nc[0] == '1');
+        const char *nm = getenv("RS_MI355X_NO_MONO");
+        ctx->mono = !(nm && nm[0] == '1');
+        const char *ma = getenv("RS_MI355X_MONO_ALL");
+        ctx->mono_all = ma && ma[0] == '1';
+        if (const char *mp = getenv("RS_MI355X_MONO_MAX_PACKS")) ctx->mono_max_packs = uint32_t(strtoul(mp, nullptr, 10));
         return RS_OK;
     });
     if (st != RS_OK) {
@@ -658,6 +760,8 @@ void rs_context_destroy(rs_context *ctx) {
     if (ctx->d_lut) (void)hipFree(ctx->d_lut);
     if (ctx->d_lwfold) (void)hipFree(ctx->d_lwfold);
     if (ctx->d_sync) (void)hipFree(ctx->d_sync);
+    for (uint32_t *p : ctx->d_img)
+        if (p) (void)hipFree(p);
     if (ctx->d_fault) (void)hipFree(ctx->d_fault);
     delete ctx;
 }
@@ -1086,6 +1190,14 @@ rs_status rs_chain_enable(rs_context *ctx, int enable) {
     if (!ctx) return RS_ERR_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> lock(ctx->mu);
     ctx->chain = enable != 0;
+    return RS_OK;
+}
+
+rs_status rs_mono_enable(rs_context *ctx, int enable) {
+    if (!ctx) return RS_ERR_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    ctx->mono = enable != 0;
+    ctx->mono_all = enable == 2;
     return RS_OK;
 }
 

@@ -100,6 +100,33 @@ struct ChainArgs {
 // hipErrorNotSupported: no chain kernel for this (K0, K1, spl).
 hipError_t launch_chain(int mode, int K0, int K1, int spl, const ChainArgs &C, hipStream_t stream);
 
+// Column kernel (DESIGN.md "Column kernel"): one workgroup owns ALL n = 2^L
+// transform rows of one pack (4 elements of every row), so a whole encode or
+// decode runs without any cross-workgroup exchange.  Twiddles come from
+// layer-ordered images: image t (transform skew offset t * n) holds, for
+// layer b = 0..L-1 and group g < n / 2^(b+1), the perm table of skew index
+// g * 2^(b+1) + 2^b + t * n - 1 at table slot n - n / 2^b + g.
+enum MonoMode { kMonoEncodeHigh = 0, kMonoEncodeLow = 1, kMonoDecode = 2 };
+struct MonoArgs {
+    uint32_t packs = 0;          // packs per row (shard_bytes / 8, rounded up)
+    uint32_t packs_per_xcd = 0;  // ceil(packs / 8): workgroup b runs pack (b % 8) * packs_per_xcd + b / 8
+    RowMap src[2];               // transform rows to load (others are zero)
+    uint32_t nsrc = 0;
+    RowMap dst;                  // transform rows to store (decode: erased originals only)
+    uint32_t chunks = 1;         // high: IFFT chunks XOR-folded; low: FFT output chunks
+    const uint32_t *img = nullptr;  // twiddle images of this L, image t at img + t * img_words
+    uint64_t img_words = 0;         // (n - 1) * 20
+    uint32_t ifft_img = 0, ifft_img_step = 0;  // image of IFFT chunk c: ifft_img + c * ifft_img_step
+    uint32_t fft_img = 0, fft_img_step = 0;
+    const uint32_t *rowinfo = nullptr;  // decode: bits 0-15 log factor, bit 16 erased
+    const uint32_t *lut = nullptr;      // perm tables by log factor (Engine::mul semantics)
+};
+// hipErrorNotSupported: no column kernel for this L (7 <= L <= 12 are built).
+hipError_t launch_mono(int mode, int L, const MonoArgs &A, hipStream_t stream);
+// Variant launch_mono picks: LDS-staged twiddles (single chunk, 2 rows per lane).
+bool mono_staged(int L, uint32_t chunks);
+int mono_rows_log2_per_lane(int L);
+
 // eval_poly for a decode: erasure vector -> per-row log factors.
 //   state[r] (r < 2^u): bit0 = erasure-vector entry, bit1 = row received.
 //   low_rate: the erasure vector is also 1 on [2^u, 65536) (rate_low.rs:196).

@@ -1,0 +1,813 @@
+// Column kernel ("mono") of the MI355X Reed-Solomon engine.
+//
+// One workgroup owns every one of the n = 2^L transform rows of ONE pack (4
+// GF(2^16) elements: 4 low bytes at block offset 4p, 4 high bytes at 32 + 4p,
+// reference layout src/algorithm.md:18-31).  Every engine op is column-wise
+// (src/engine/utils.rs:35-43, src/engine/engine_naive.rs:107-146), so the
+// whole encode -- IFFT (engine_naive.rs:75-105), chunk XOR-fold / replicate
+// (rate_high.rs:56-74, rate_low.rs:59-78), FFT (engine_naive.rs:43-73) -- or
+// decode (rate_high.rs:172-254) runs inside one workgroup: there is no
+// cross-workgroup hand-off, which is what bounds the multi-pass / chain
+// kernels at small shard matrices (DESIGN.md "Column kernel").
+//
+// Rows live in registers: a lane holds R = 2^LR rows; row-index bits are
+// spread over register bits, the 6 lane bits and the wave bits.  A butterfly
+// layer on row bit x needs x in a register bit; it gets there by a 2x2
+// register/lane transpose (DPP, ds_swizzle or v_permlane{16,32}_swap -- no
+// LDS traffic, no barrier) or, for wave bits, by one LDS remap of the whole
+// column (twice per transform pair).  The plan (which bit sits where before
+// every op) is computed at compile time.
+//
+// Twiddle tables are read straight from layer-ordered images (rs_device.hpp)
+// into registers, one layer ahead of use, so table latency hides behind the
+// butterflies of the current layer.
+#include <hip/hip_runtime.h>
+
+#include "rs_device.hpp"
+#include "rs_gf.hpp"
+
+namespace rs {
+namespace {
+
+#ifdef RS_MONO_STAMPS  // tools/mono_probe.hip: per-workgroup timestamps (waits for memory first)
+__device__ uint64_t g_mono_stamps[4096][16];
+#define RS_MSTAMP(i)                                                                                 \
+    do {                                                                                             \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                  \
+        if (threadIdx.x == 0 && blockIdx.x < 4096) g_mono_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define RS_MSTAMP(i)
+#endif
+
+// ---------------------------------------------------------------------------
+// compile-time plan
+
+struct Map {
+    int reg[3];   // row bit held by register-index bit s
+    int lane[6];  // row bit held by lane bit j
+    int wave[4];  // row bit held by wave bit k
+};
+enum : int { kOpLayer = 1, kOpXpose = 2, kOpRemap = 3 };
+struct Op {
+    int kind, bit, rs, ls;  // layer on `bit` (register bit rs) / swap register bit rs with lane bit ls
+};
+constexpr int kMaxOps = 64;
+struct Seq {
+    int count = 0;
+    Op ops[kMaxOps] = {};
+    Map maps[kMaxOps + 1] = {};  // maps[i]: placement before op i; maps[count]: final
+};
+
+constexpr int find_reg(const Map &m, int LR, int x) {
+    for (int s = 0; s < LR; ++s)
+        if (m.reg[s] == x) return s;
+    return -1;
+}
+constexpr int find_lane(const Map &m, int x) {
+    for (int j = 0; j < 6; ++j)
+        if (m.lane[j] == x) return j;
+    return -1;
+}
+constexpr int next_use(const int *bits, int nb, int from, int x) {
+    for (int t = from; t < nb; ++t)
+        if (bits[t] == x) return t;
+    return 1 << 20;
+}
+constexpr void push(Seq &s, Op op, const Map &after) {
+    s.ops[s.count] = op;
+    ++s.count;
+    s.maps[s.count] = after;
+}
+
+// Butterfly layers on `bits` in order; a bit not in a register is swapped in
+// from its lane bit, evicting the register bit used furthest in the future.
+constexpr void layers(Seq &s, Map &m, int LR, const int *bits, int nb) {
+    for (int t = 0; t < nb; ++t) {
+        const int x = bits[t];
+        int rs = find_reg(m, LR, x);
+        if (rs < 0) {
+            const int j = find_lane(m, x);
+            int far = -1;
+            for (int q = 0; q < LR; ++q) {
+                const int u = next_use(bits, nb, t + 1, m.reg[q]);
+                if (u > far) far = u, rs = q;
+            }
+            const int tmp = m.reg[rs];
+            m.reg[rs] = m.lane[j];
+            m.lane[j] = tmp;
+            push(s, Op{kOpXpose, x, rs, j}, m);
+        }
+        push(s, Op{kOpLayer, x, rs, 0}, m);
+    }
+}
+
+// Placement of a segment: in-wave bits [lo, lo + IW), wave bits the rest.
+// Registers take the first bits of `order`; lane bits the next ones, cheapest
+// transposes (permlane swaps: lane bits 5, 4; DPP: 0, 1, 3; swizzle: 2) first.
+constexpr Map seg_map(int L, int LR, int lo, const int *order, int no) {
+    const int IW = LR + 6;
+    int pri[16] = {}, np = 0;
+    for (int t = 0; t < no; ++t) {
+        const int x = order[t];
+        bool seen = x < lo || x >= lo + IW;
+        for (int q = 0; q < np; ++q) seen = seen || pri[q] == x;
+        if (!seen) pri[np++] = x;
+    }
+    for (int x = lo; x < lo + IW; ++x) {
+        bool seen = false;
+        for (int q = 0; q < np; ++q) seen = seen || pri[q] == x;
+        if (!seen) pri[np++] = x;
+    }
+    const int pref[6] = {5, 4, 0, 1, 3, 2};
+    Map m{};
+    for (int s = 0; s < 3; ++s) m.reg[s] = s < LR ? pri[s] : -1;
+    for (int j = 0; j < 6; ++j) m.lane[pref[j]] = pri[LR + j];
+    int k = 0;
+    for (int x = 0; x < L; ++x)
+        if (x < lo || x >= lo + IW) m.wave[k++] = x;
+    for (; k < 4; ++k) m.wave[k] = -1;
+    return m;
+}
+
+template <int L, int LR>
+struct Plan {
+    static constexpr int IW = LR + 6, WB = L - IW, R = 1 << LR;
+    static_assert(WB >= 0 && WB <= 4, "column kernel: 6 lane bits + LR register bits + up to 4 wave bits");
+
+    static constexpr Seq make_ifft() {
+        Seq s{};
+        int bits[16] = {}, order[32] = {}, no = 0;
+        if (WB == 0) {
+            for (int x = 0; x < L; ++x) order[no++] = x;
+            for (int x = L - 1; x >= 0; --x) order[no++] = x;
+            Map m = seg_map(L, LR, 0, order, no);
+            s.maps[0] = m;
+            for (int x = 0; x < L; ++x) bits[x] = x;
+            layers(s, m, LR, bits, L);
+            return s;
+        }
+        // segment A: IFFT layers 0..IW-1 with the low bits in-wave
+        for (int x = 0; x < IW; ++x) order[no++] = x, bits[x] = x;
+        Map m = seg_map(L, LR, 0, order, no);
+        s.maps[0] = m;
+        layers(s, m, LR, bits, IW);
+        // segment B: the top IW bits in-wave: IFFT layers IW..L-1 (then FFT L-1..WB)
+        no = 0;
+        for (int x = IW; x < L; ++x) order[no++] = x;
+        for (int x = L - 1; x >= WB; --x) order[no++] = x;
+        m = seg_map(L, LR, WB, order, no);
+        push(s, Op{kOpRemap, -1, 0, 0}, m);
+        for (int x = IW; x < L; ++x) bits[x - IW] = x;
+        layers(s, m, LR, bits, L - IW);
+        return s;
+    }
+    static constexpr Seq ifft = make_ifft();
+
+    static constexpr Seq make_fft() {
+        Seq s{};
+        int bits[16] = {}, order[16] = {}, no = 0;
+        Map m = ifft.maps[ifft.count];
+        s.maps[0] = m;
+        const int stop = WB;  // FFT layers L-1..stop in the IFFT's final placement
+        for (int x = L - 1; x >= stop; --x) bits[L - 1 - x] = x;
+        layers(s, m, LR, bits, L - stop);
+        if (WB == 0) return s;
+        // segment C: the low IW bits in-wave again, FFT layers WB-1..0
+        for (int x = WB - 1; x >= 0; --x) order[no++] = x;
+        m = seg_map(L, LR, 0, order, no);
+        push(s, Op{kOpRemap, -1, 0, 0}, m);
+        for (int x = WB - 1; x >= 0; --x) bits[WB - 1 - x] = x;
+        layers(s, m, LR, bits, WB);
+        return s;
+    }
+    static constexpr Seq fft = make_fft();
+};
+
+template <int L, int LR, bool FFT>
+struct SeqOf {
+    static constexpr const Seq &v = FFT ? Plan<L, LR>::fft : Plan<L, LR>::ifft;
+};
+
+constexpr int layer_ordinal(const Seq &s, int i) {
+    int k = 0;
+    for (int q = 0; q < i; ++q) k += s.ops[q].kind == kOpLayer;
+    return k;
+}
+
+// ---------------------------------------------------------------------------
+// device helpers
+
+// Row index of register i under placement maps[I] of sequence S.
+template <typename S, int I>
+__device__ __forceinline__ uint32_t lane_rows(uint32_t lane, uint32_t wave) {
+    constexpr Map m = S::v.maps[I];
+    uint32_t r = 0;
+    static_for<0, 6>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        r |= ((lane >> j) & 1u) << m.lane[j];
+    });
+    static_for<0, 4>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if constexpr (m.wave[k] >= 0) r |= ((wave >> k) & 1u) << m.wave[k];
+    });
+    return r;
+}
+template <typename S, int I, int LR>
+__device__ __forceinline__ constexpr uint32_t reg_rows(int i) {
+    constexpr Map m = S::v.maps[I];
+    uint32_t r = 0;
+    for (int s = 0; s < LR; ++s) r |= uint32_t((i >> s) & 1) << m.reg[s];
+    return r;
+}
+
+// LDS column plane: low words at [0, n), high words at [n, 2n); the index is
+// XOR-swizzled inside 32-word runs against strided lane access.
+template <int L>
+__device__ __forceinline__ uint32_t swz(uint32_t r) {
+    return r ^ ((r >> 5) & 31u);
+}
+
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+    if constexpr (J == 0) return __builtin_amdgcn_update_dpp(0, int(v), 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+    else if constexpr (J == 1) return __builtin_amdgcn_update_dpp(0, int(v), 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+    else if constexpr (J == 2) return __builtin_amdgcn_ds_swizzle(int(v), 0x101F);  // lane ^ 4
+    else return __builtin_amdgcn_update_dpp(0, int(v), 0x128, 0xF, 0xF, false);  // row_ror:8 = lane ^ 8
+}
+
+// 2x2 transpose of (register pair, lane bit J): the lane with bit J clear ends
+// with (a, partner's a), its partner with (a-lane's b, b).
+template <int J>
+__device__ __forceinline__ void xpose(uint32_t &a, uint32_t &b, uint32_t lane) {
+    if constexpr (J == 4) {
+        const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+        a = r[0];
+        b = r[1];
+    } else if constexpr (J == 5) {
+        const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+        a = r[0];
+        b = r[1];
+    } else {
+        const bool up = (lane >> J) & 1u;
+        const uint32_t recv = xor_lane<J>(up ? a : b);
+        if (up) a = recv;
+        else b = recv;
+    }
+}
+
+template <int L, int LR>
+struct Col {
+    static constexpr int R = 1 << LR;
+    static constexpr uint32_t n = 1u << L;
+    uint32_t lo[R], hi[R];
+};
+
+// Index of register pair (i, i | 2^s) among the pairs of register bit s.
+constexpr int pair_of(int i, int s) { return (i & ((1 << s) - 1)) | ((i >> (s + 1)) << s); }
+
+// The perm table of the butterfly group of row `row` at layer x.
+__device__ __forceinline__ void load_tab(const uint32_t *img, int L, int x, uint32_t row, uint32_t (&t)[20]) {
+    const uint32_t n = 1u << L;
+    const uint32_t slot = n - (n >> x) + (row >> (x + 1));
+#ifdef RS_MONO_FAKE_TABS  // tools/mono_probe.hip: tables without memory traffic
+    for (int q = 0; q < 20; ++q) t[q] = slot * 0x01010101u + q;
+    return;
+#endif
+    const uint4 *p = reinterpret_cast<const uint4 *>(img) + slot * 5u;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        const uint4 v = p[q];
+        t[4 * q] = v.x, t[4 * q + 1] = v.y, t[4 * q + 2] = v.z, t[4 * q + 3] = v.w;
+    }
+}
+
+// Table source: the layer-ordered image in global memory (through L1).
+struct GlobalTabs {
+    const uint32_t *img;
+    template <int L, int LR, typename S, int I, int PH>
+    __device__ __forceinline__ void get(int x, uint32_t row, uint32_t (&t)[20]) const {
+        load_tab(img, L, x, row, t);
+    }
+};
+
+template <int L, int LR>
+struct Stage {
+    static constexpr int IW = LR + 6, WB = L - IW;
+    static constexpr uint32_t n = 1u << L, W = 1u << IW;
+    // layers of the last (FFT) in-wave phase
+    static constexpr int NB3 = WB > 0 ? WB : L;
+    static constexpr uint32_t kPriv = W - 1;                       // tables per wave region
+    static constexpr uint32_t kP3 = W - (W >> NB3);                  // tables of phase 3
+    static constexpr uint32_t kShI = WB > 0 ? (n >> IW) - 1 : 0;     // shared: IFFT layers IW..L-1
+    static constexpr uint32_t kShF = WB > 0 ? (n >> WB) - 1 : 0;     // shared: FFT layers WB..L-1
+    static constexpr uint32_t kShared = kShI + kShF;
+    static constexpr uint32_t kWaves = 1u << (L - LR - 6);
+    static constexpr uint32_t plane_words = 2 * n;
+    static constexpr uint32_t words = plane_words + (kShared + kWaves * kPriv) * 20;
+};
+
+// Table source: tables staged in LDS (STAGED column kernel).  Phase 1 (IFFT
+// layers with the low bits in-wave) and phase 3 (FFT layers likewise) read a
+// wave-private region: a wave's rows there are 2^IW consecutive rows, so its
+// groups are its own.  Phase 2 (top bits in-wave, wave bits low) reads the
+// region shared by all waves.
+template <int L, int LR>
+struct LdsTabs {
+    using G = Stage<L, LR>;
+    const uint32_t *priv, *shared;
+    template <int, int, typename S, int I, int PH>
+    __device__ __forceinline__ void get(int x, uint32_t row, uint32_t (&t)[20]) const {
+        uint32_t slot;
+        const uint32_t *base;
+        if constexpr (PH == 1 || PH == 3) {
+            slot = G::W - (G::W >> x) + ((row & (G::W - 1)) >> (x + 1));
+            base = priv;
+        } else if constexpr (PH == 2) {
+            slot = (G::n >> G::IW) - (G::n >> x) + (row >> (x + 1));
+            base = shared;
+        } else {
+            slot = G::kShI + (G::n >> G::WB) - (G::n >> x) + (row >> (x + 1));
+            base = shared;
+        }
+        const uint4 *p = reinterpret_cast<const uint4 *>(base) + slot * 5u;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const uint4 v = p[q];
+            t[4 * q] = v.x, t[4 * q + 1] = v.y, t[4 * q + 2] = v.z, t[4 * q + 3] = v.w;
+        }
+    }
+};
+
+// Phase of op I of a sequence: 1 = IFFT in-wave low bits, 2 = IFFT top bits,
+// 4 = FFT top bits (shared region, FFT part), 3 = FFT in-wave low bits.
+constexpr int remap_index(const Seq &s) {
+    for (int i = 0; i < s.count; ++i)
+        if (s.ops[i].kind == kOpRemap) return i;
+    return s.count;
+}
+template <typename S, bool FFT, int I>
+constexpr int phase_of() {
+    constexpr int ri = remap_index(S::v);
+    if constexpr (ri == S::v.count) return FFT ? 3 : 1;  // one segment (no wave bits)
+    else if constexpr (FFT) return I < ri ? 4 : 3;
+    else return I < ri ? 1 : 2;
+}
+
+template <int L, int LR, typename S, int I, bool FFT, typename TS>
+__device__ __forceinline__ void load_layer_tabs(const TS &ts, uint32_t lane, uint32_t wave,
+                                                uint32_t (&t)[(1 << LR) / 2][20]) {
+    constexpr Op op = S::v.ops[I];
+    const uint32_t lr = lane_rows<S, I>(lane, wave);
+    static_for<0, (1 << LR)>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (!((i >> op.rs) & 1))
+            ts.template get<L, LR, S, I, phase_of<S, FFT, I>()>(op.bit, lr | reg_rows<S, I, LR>(i),
+                                                                t[pair_of(i, op.rs)]);
+    });
+}
+
+template <int L, int LR, typename S, int I, bool IFFT>
+__device__ __forceinline__ void apply_layer(const uint32_t (&t)[(1 << LR) / 2][20], Col<L, LR> &c) {
+    constexpr Op op = S::v.ops[I];
+    static_for<0, (1 << LR)>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int i2 = i | (1 << op.rs);
+        if constexpr (!((i >> op.rs) & 1)) {
+            if constexpr (IFFT) ifft_bfly(c.lo[i], c.hi[i], c.lo[i2], c.hi[i2], t[pair_of(i, op.rs)]);
+            else fft_bfly(c.lo[i], c.hi[i], c.lo[i2], c.hi[i2], t[pair_of(i, op.rs)]);
+        }
+    });
+}
+
+template <int L, int LR, typename S, int I>
+__device__ __forceinline__ void apply_xpose(Col<L, LR> &c, uint32_t lane) {
+    constexpr Op op = S::v.ops[I];
+    static_for<0, (1 << LR)>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int i2 = i | (1 << op.rs);
+        if constexpr (!((i >> op.rs) & 1)) {
+            xpose<op.ls>(c.lo[i], c.lo[i2], lane);
+            xpose<op.ls>(c.hi[i], c.hi[i2], lane);
+        }
+    });
+}
+
+// Whole-column exchange through LDS from placement maps[I] to maps[I + 1].
+template <int L, int LR, typename S, int I>
+__device__ __forceinline__ void apply_remap(Col<L, LR> &c, uint32_t *plane, uint32_t lane, uint32_t wave) {
+    constexpr uint32_t n = 1u << L;
+    __syncthreads();
+    const uint32_t a = lane_rows<S, I>(lane, wave);
+    static_for<0, (1 << LR)>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const uint32_t x = swz<L>(a | reg_rows<S, I, LR>(i));
+        plane[x] = c.lo[i];
+        plane[n + x] = c.hi[i];
+    });
+    __syncthreads();
+    const uint32_t b = lane_rows<S, I + 1>(lane, wave);
+    static_for<0, (1 << LR)>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const uint32_t x = swz<L>(b | reg_rows<S, I + 1, LR>(i));
+        c.lo[i] = plane[x];
+        c.hi[i] = plane[n + x];
+    });
+}
+
+constexpr int layer_at(const Seq &s, int k) {
+    for (int i = 0; i < s.count; ++i)
+        if (s.ops[i].kind == kOpLayer && k-- == 0) return i;
+    return s.count;
+}
+constexpr int num_layers(const Seq &s) { return layer_ordinal(s, s.count); }
+
+#ifndef RS_MONO_PF
+#define RS_MONO_PF 3
+#endif
+// Layers of twiddle tables in flight ahead of the layer being computed.
+constexpr int kMonoPrefetch = RS_MONO_PF;
+
+// Run one transform sequence.  The tables of layer k + B are requested right
+// after layer k, into the registers layer k just released, so table latency
+// hides behind B - 1 layers of butterflies.  Requests never cross the remap:
+// the tables beyond it may not be in place yet (staged kernel).  `pre_remap`
+// runs just before the remap.
+template <int L, int LR, bool FFT, int B0, typename TS, typename PreRemap>
+__device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR> &c, uint32_t *plane, uint32_t lane, uint32_t wave,
+                                        const PreRemap &pre_remap) {
+    using S = SeqOf<L, LR, FFT>;
+    constexpr int NT = (1 << LR) / 2;
+    constexpr int NL = num_layers(S::v);
+    constexpr int RI = remap_index(S::v);
+    constexpr int NL1 = layer_ordinal(S::v, RI);  // layers before the remap
+    constexpr int B = B0 < NL ? B0 : NL;
+    uint32_t tb[B][NT][20];
+    // first tables of a segment [k0, k1) of layer ordinals
+    auto prime = [&](auto k0c, auto k1c) {
+        constexpr int k0 = decltype(k0c)::value, k1 = decltype(k1c)::value;
+        static_for<k0, (k0 + B < k1 ? k0 + B : k1)>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            load_layer_tabs<L, LR, S, layer_at(S::v, k), FFT>(ts, lane, wave, tb[k % B]);
+        });
+    };
+    prime(std::integral_constant<int, 0>{}, std::integral_constant<int, NL1>{});
+    static_for<0, S::v.count>([&](auto ic) {
+        constexpr int I = decltype(ic)::value;
+        constexpr Op op = S::v.ops[I];
+        if constexpr (op.kind == kOpXpose) {
+            apply_xpose<L, LR, S, I>(c, lane);
+        } else if constexpr (op.kind == kOpRemap) {
+            pre_remap();
+            RS_MSTAMP(FFT ? 8 : 3);
+            apply_remap<L, LR, S, I>(c, plane, lane, wave);
+            RS_MSTAMP(FFT ? 9 : 4);
+            prime(std::integral_constant<int, NL1>{}, std::integral_constant<int, NL>{});
+        } else {
+            constexpr int k = layer_ordinal(S::v, I);
+#ifndef RS_MONO_SKIP_LAYERS
+            apply_layer<L, LR, S, I, !FFT>(tb[k % B], c);
+#endif
+            constexpr int end = k < NL1 ? NL1 : NL;
+            if constexpr (k + B < end) {
+                load_layer_tabs<L, LR, S, layer_at(S::v, k + B), FFT>(ts, lane, wave, tb[k % B]);
+                asm volatile("" ::: "memory");  // keep the request here, ahead of its use
+            }
+        }
+    });
+}
+
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
+
+__device__ __forceinline__ const uint8_t *row_ptr(const MonoArgs &A, uint32_t r) {
+    const uint8_t *p = nullptr;
+    if (r >= A.src[0].row_begin && r < A.src[0].row_end)
+        p = A.src[0].base + uint64_t(r - A.src[0].row_begin) * A.src[0].stride;
+    if (A.nsrc > 1 && r >= A.src[1].row_begin && r < A.src[1].row_end)
+        p = A.src[1].base + uint64_t(r - A.src[1].row_begin) * A.src[1].stride;
+    return p;
+}
+
+// Load transform rows `chunk * n + row` (placement: start of the IFFT).
+// SCALE (decode): erased rows load as zero, received rows are multiplied by
+// exp(log factor) (rate_high.rs:213-231).
+template <int L, int LR, bool SCALE>
+__device__ __forceinline__ void load_col(const MonoArgs &A, uint32_t chunk, uint32_t pk_off, Col<L, LR> &c,
+                                         uint32_t lane, uint32_t wave) {
+    using S = SeqOf<L, LR, false>;
+    const uint32_t a = lane_rows<S, 0>(lane, wave) + chunk * (1u << L);
+    uint32_t f[1 << LR];
+    static_for<0, (1 << LR)>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const uint32_t r = a | reg_rows<S, 0, LR>(i);
+        const uint8_t *p = row_ptr(A, r);
+        if constexpr (SCALE) {
+            f[i] = A.rowinfo[r];
+            if (f[i] & 0x10000u) p = nullptr;
+        }
+        uint32_t l = 0, h = 0;
+#ifdef RS_MONO_SKIP_IO
+        p = nullptr;
+        l = r * 0x9E3779B9u, h = r;
+#endif
+        if (p) {
+            l = *reinterpret_cast<const uint32_t *>(p + pk_off);
+            h = *reinterpret_cast<const uint32_t *>(p + pk_off + 32);
+        }
+        c.lo[i] = l;
+        c.hi[i] = h;
+    });
+    if constexpr (SCALE) {
+        static_for<0, (1 << LR)>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            uint32_t t[20];
+            const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + (f[i] & 0xFFFFu) * 5u;
+#pragma unroll
+            for (int w = 0; w < 5; ++w) {
+                const uint4 v = q[w];
+                t[4 * w] = v.x, t[4 * w + 1] = v.y, t[4 * w + 2] = v.z, t[4 * w + 3] = v.w;
+            }
+            gf_mul4(c.lo[i], c.hi[i], t);
+        });
+    }
+}
+
+// Store transform rows `chunk * n + row` that fall in A.dst (placement: end
+// of the FFT).  REVEAL (decode): only erased rows, multiplied by
+// exp(65535 - log factor) (rate_high.rs:241-245).
+template <int L, int LR, bool REVEAL>
+__device__ __forceinline__ void store_col(const MonoArgs &A, uint32_t chunk, uint32_t pk_off, Col<L, LR> &c,
+                                          uint32_t lane, uint32_t wave) {
+    using S = SeqOf<L, LR, true>;
+    const uint32_t a = lane_rows<S, S::v.count>(lane, wave) + chunk * (1u << L);
+    static_for<0, (1 << LR)>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const uint32_t r = a | reg_rows<S, S::v.count, LR>(i);
+        if (r >= A.dst.row_begin && r < A.dst.row_end) {
+            uint8_t *p = const_cast<uint8_t *>(A.dst.base) + uint64_t(r - A.dst.row_begin) * A.dst.stride + pk_off;
+            uint32_t l = c.lo[i], h = c.hi[i];
+            bool keep = true;
+            if constexpr (REVEAL) {
+                const uint32_t f = A.rowinfo[r];
+                keep = f & 0x10000u;
+                if (keep) {
+                    uint32_t t[20];
+                    const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + (65535u - (f & 0xFFFFu)) * 5u;
+#pragma unroll
+                    for (int w = 0; w < 5; ++w) {
+                        const uint4 v = q[w];
+                        t[4 * w] = v.x, t[4 * w + 1] = v.y, t[4 * w + 2] = v.z, t[4 * w + 3] = v.w;
+                    }
+                    gf_mul4(l, h, t);
+                }
+            }
+#ifdef RS_MONO_SKIP_IO
+            keep = (l ^ h) == 0x12345678u;
+#endif
+            if (keep) {
+                *reinterpret_cast<uint32_t *>(p) = l;
+                *reinterpret_cast<uint32_t *>(p + 32) = h;
+            }
+        }
+    });
+}
+
+// Formal derivative, closed form over the whole column (src/engine/utils.rs:99-104):
+//   out[q] = x[q] ^ XOR_{b < L, q_b = 0} x[q | 2^b]   (placement: end of the IFFT)
+template <int L, int LR>
+__device__ __forceinline__ void formal_derivative(Col<L, LR> &c, uint32_t *plane, uint32_t lane, uint32_t wave) {
+    using S = SeqOf<L, LR, true>;
+    constexpr uint32_t n = 1u << L;
+    const uint32_t a = lane_rows<S, 0>(lane, wave);
+    __syncthreads();
+    static_for<0, (1 << LR)>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const uint32_t x = swz<L>(a | reg_rows<S, 0, LR>(i));
+        plane[x] = c.lo[i];
+        plane[n + x] = c.hi[i];
+    });
+    __syncthreads();
+    static_for<0, (1 << LR)>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const uint32_t q = a | reg_rows<S, 0, LR>(i);
+        uint32_t l = c.lo[i], h = c.hi[i];
+#pragma unroll
+        for (int b = 0; b < L; ++b)
+            if (!(q & (1u << b))) {
+                const uint32_t x = swz<L>(q | (1u << b));
+                l ^= plane[x];
+                h ^= plane[n + x];
+            }
+        c.lo[i] = l;
+        c.hi[i] = h;
+    });
+}
+
+// ---------------------------------------------------------------------------
+// LDS staging of the twiddle tables (STAGED kernel): 16-byte pieces q of the
+// wave-private region (phase 1 from the IFFT image, phase 3 from the FFT
+// image) and of the shared region.
+template <int L, int LR>
+__device__ __forceinline__ uint4 priv_piece(const uint32_t *img, uint32_t wave, uint32_t q) {
+    using G = Stage<L, LR>;
+    const uint32_t t = q / 5, piece = q - t * 5;
+    const uint32_t y = G::W - t;                              // in [1, W]
+    const int b = G::IW - int(32 - __builtin_clz(y - 1));    // IW - ceil(log2 y)
+    const uint32_t local = t - (G::W - (G::W >> b));
+    const uint32_t slot = G::n - (G::n >> b) + wave * (G::W >> (b + 1)) + local;
+    return reinterpret_cast<const uint4 *>(img)[slot * 5u + piece];
+}
+template <int L, int LR>
+__device__ __forceinline__ uint4 shared_piece(const uint32_t *img_i, const uint32_t *img_f, uint32_t q) {
+    using G = Stage<L, LR>;
+    const uint32_t t = q / 5, piece = q - t * 5;
+    const uint32_t slot = t < G::kShI ? G::n - (G::n >> G::IW) + t : G::n - (G::n >> G::WB) + (t - G::kShI);
+    return reinterpret_cast<const uint4 *>(t < G::kShI ? img_i : img_f)[slot * 5u + piece];
+}
+
+#ifndef RS_MONO_LDS_PF
+#define RS_MONO_LDS_PF 2
+#endif
+
+template <int L, int LR, int MODE, bool STAGED>
+__global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
+    using C = Col<L, LR>;
+    using G = Stage<L, LR>;
+    constexpr int R = 1 << LR;
+    constexpr uint32_t T = 1u << (L - LR);
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t *plane = lds;
+    // XCD-aware: workgroup b runs on XCD b % 8, so the 8 packs of one 64-byte
+    // block (which share cache lines) go to one XCD's L2.
+    const uint32_t b = blockIdx.x;
+    const uint32_t pk = (b & 7u) * A.packs_per_xcd + (b >> 3);
+    if (pk >= A.packs) return;
+    const uint32_t pk_off = (pk >> 3) * 64u + (pk & 7u) * 4u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t *img_i = A.img + uint64_t(A.ifft_img) * A.img_words;
+    const uint32_t *img_f = A.img + uint64_t(A.fft_img) * A.img_words;
+    C c;
+    if constexpr (STAGED) {
+        // one chunk in, one chunk out; every table read comes from LDS
+        constexpr bool DEC = MODE == kMonoDecode;
+        RS_MSTAMP(0);
+        load_col<L, LR, DEC>(A, 0, pk_off, c, lane, wave);
+        uint32_t *shared = lds + G::plane_words;
+        uint32_t *priv = shared + G::kShared * 20 + wave * G::kPriv * 20;
+        constexpr int KP1 = (5 * G::kPriv + 63) / 64, KP3 = (5 * G::kP3 + 63) / 64;
+        constexpr int KSH = G::kShared ? (5 * G::kShared + T - 1) / T : 1;
+        {
+            uint4 v1[KP1], vs[KSH];
+            static_for<0, KP1>([&](auto kc) {
+                const uint32_t q = lane + 64u * decltype(kc)::value;
+                if (q < 5 * G::kPriv) v1[kc] = priv_piece<L, LR>(img_i, wave, q);
+            });
+            static_for<0, KSH>([&](auto kc) {
+                const uint32_t q = threadIdx.x + T * decltype(kc)::value;
+                if (q < 5 * G::kShared) vs[kc] = shared_piece<L, LR>(img_i, img_f, q);
+            });
+            static_for<0, KP1>([&](auto kc) {
+                const uint32_t q = lane + 64u * decltype(kc)::value;
+                if (q < 5 * G::kPriv) reinterpret_cast<uint4 *>(priv)[q] = v1[kc];
+            });
+            static_for<0, KSH>([&](auto kc) {
+                const uint32_t q = threadIdx.x + T * decltype(kc)::value;
+                if (q < 5 * G::kShared) reinterpret_cast<uint4 *>(shared)[q] = vs[kc];
+            });
+        }
+        RS_MSTAMP(1);
+        const LdsTabs<L, LR> ts{priv, shared};
+        // phase-3 tables: requested when phase 1 ends, written over this wave's
+        // phase-1 tables when phase 2 ends
+        uint4 v3[KP3];
+        auto issue3 = [&]() {
+            static_for<0, KP3>([&](auto kc) {
+                const uint32_t q = lane + 64u * decltype(kc)::value;
+                if (q < 5 * G::kP3) v3[kc] = priv_piece<L, LR>(img_f, wave, q);
+            });
+        };
+        auto write3 = [&]() {
+            static_for<0, KP3>([&](auto kc) {
+                const uint32_t q = lane + 64u * decltype(kc)::value;
+                if (q < 5 * G::kP3) reinterpret_cast<uint4 *>(priv)[q] = v3[kc];
+            });
+        };
+        if constexpr (G::WB > 0) {
+            run_seq<L, LR, false, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, issue3);
+            RS_MSTAMP(5);
+            if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
+            run_seq<L, LR, true, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, write3);
+        } else {
+            run_seq<L, LR, false, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, NoHook{});
+            issue3();
+            if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
+            write3();
+            run_seq<L, LR, true, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, NoHook{});
+        }
+        RS_MSTAMP(10);
+        store_col<L, LR, DEC>(A, 0, pk_off, c, lane, wave);
+        RS_MSTAMP(11);
+    } else if constexpr (MODE == kMonoEncodeHigh) {
+        // rate_high.rs:44-87: recovery = FFT_0(XOR_c IFFT_{c n + n}(chunk c))
+        load_col<L, LR, false>(A, 0, pk_off, c, lane, wave);
+        run_seq<L, LR, false, kMonoPrefetch>(GlobalTabs{img_i}, c, plane, lane, wave, NoHook{});
+        for (uint32_t ch = 1; ch < A.chunks; ++ch) {
+            C t;
+            load_col<L, LR, false>(A, ch, pk_off, t, lane, wave);
+            run_seq<L, LR, false, kMonoPrefetch>(
+                GlobalTabs{img_i + uint64_t(ch) * A.ifft_img_step * A.img_words}, t, plane, lane, wave, NoHook{});
+            static_for<0, R>([&](auto ic) {
+                c.lo[ic] ^= t.lo[ic];
+                c.hi[ic] ^= t.hi[ic];
+            });
+        }
+        run_seq<L, LR, true, kMonoPrefetch>(GlobalTabs{img_f}, c, plane, lane, wave, NoHook{});
+        store_col<L, LR, false>(A, 0, pk_off, c, lane, wave);
+    } else if constexpr (MODE == kMonoEncodeLow) {
+        // rate_low.rs:44-87: recovery chunk c = FFT_{c n + n}(IFFT_0(original))
+        load_col<L, LR, false>(A, 0, pk_off, c, lane, wave);
+        run_seq<L, LR, false, kMonoPrefetch>(GlobalTabs{img_i}, c, plane, lane, wave, NoHook{});
+        for (uint32_t ch = 0; ch < A.chunks; ++ch) {
+            C t = c;
+            run_seq<L, LR, true, kMonoPrefetch>(
+                GlobalTabs{img_f + uint64_t(ch) * A.fft_img_step * A.img_words}, t, plane, lane, wave, NoHook{});
+            store_col<L, LR, false>(A, ch, pk_off, t, lane, wave);
+        }
+    } else {
+        // rate_high.rs:213-245 / rate_low.rs:213-245 after eval_poly
+        load_col<L, LR, true>(A, 0, pk_off, c, lane, wave);
+        run_seq<L, LR, false, kMonoPrefetch>(GlobalTabs{img_i}, c, plane, lane, wave, NoHook{});
+        formal_derivative<L, LR>(c, plane, lane, wave);
+        run_seq<L, LR, true, kMonoPrefetch>(GlobalTabs{img_f}, c, plane, lane, wave, NoHook{});
+        store_col<L, LR, true>(A, 0, pk_off, c, lane, wave);
+    }
+}
+
+#ifndef RS_MONO_LR10
+#define RS_MONO_LR10 1
+#endif
+// log2 rows per lane: 2^(L - LR) threads, at most 512
+constexpr int mono_lr(int L) { return L <= 10 ? (RS_MONO_LR10 < L - 6 ? RS_MONO_LR10 : L - 6) : L - 9; }
+
+template <int L, int MODE, bool STAGED>
+hipError_t launch_ls(const MonoArgs &A, hipStream_t s) {
+    constexpr int LR = mono_lr(L);
+    const size_t lds = STAGED ? size_t(Stage<L, LR>::words) * 4 : size_t(8) << L;
+    static bool attr_set = false;  // benign race: idempotent attribute call
+    if (!attr_set && lds > 65536) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mono<L, LR, MODE, STAGED>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    const uint32_t grid = 8u * A.packs_per_xcd;
+    k_mono<L, LR, MODE, STAGED><<<dim3(grid), 1 << (L - LR), lds, s>>>(A);
+    return hipGetLastError();
+}
+
+#ifndef RS_MONO_NO_STAGE
+#define RS_MONO_STAGED_MAX_L 10
+#else
+#define RS_MONO_STAGED_MAX_L 0
+#endif
+// Staged (LDS tables) variant: single-chunk transforms with 2 rows per lane.
+template <int L, int MODE>
+hipError_t launch_l(const MonoArgs &A, hipStream_t s) {
+    if constexpr (L <= RS_MONO_STAGED_MAX_L && mono_lr(L) == 1) {
+        if (A.chunks == 1) return launch_ls<L, MODE, true>(A, s);  // = mono_staged()
+    }
+    return launch_ls<L, MODE, false>(A, s);
+}
+
+template <int MODE>
+hipError_t launch_m(int L, const MonoArgs &A, hipStream_t s) {
+    switch (L) {
+        case 7: return launch_l<7, MODE>(A, s);
+        case 8: return launch_l<8, MODE>(A, s);
+        case 9: return launch_l<9, MODE>(A, s);
+        case 10: return launch_l<10, MODE>(A, s);
+        case 11: return launch_l<11, MODE>(A, s);
+        case 12: return launch_l<12, MODE>(A, s);
+        default: return hipErrorNotSupported;
+    }
+}
+
+}  // namespace
+
+bool mono_staged(int L, uint32_t chunks) { return L <= RS_MONO_STAGED_MAX_L && mono_lr(L) == 1 && chunks == 1; }
+int mono_rows_log2_per_lane(int L) { return mono_lr(L); }
+
+hipError_t launch_mono(int mode, int L, const MonoArgs &A, hipStream_t s) {
+    if (A.packs == 0) return hipSuccess;
+    switch (mode) {
+        case kMonoEncodeHigh: return launch_m<kMonoEncodeHigh>(L, A, s);
+        case kMonoEncodeLow: return launch_m<kMonoEncodeLow>(L, A, s);
+        case kMonoDecode: return launch_m<kMonoDecode>(L, A, s);
+        default: return hipErrorNotSupported;
+    }
+}
+
+}  // namespace rs

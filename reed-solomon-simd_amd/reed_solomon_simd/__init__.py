@@ -132,6 +132,16 @@ def chain_enable(enable: bool = True, ctx=None) -> None:
     _lib.rs_chain_enable(ctx.handle, 1 if enable else 0)
 
 
+_sig("rs_mono_enable", _int, _vp, _int)
+
+
+def mono_enable(enable=True, ctx=None) -> None:
+    """Column kernel (one workgroup per pack): False = never, True = where fastest (default),
+    2 = also multi-chunk and 2^11 / 2^12-row transforms."""
+    ctx = ctx or default_context()
+    _lib.rs_mono_enable(ctx.handle, int(enable))
+
+
 def check_device(ctx=None) -> None:
     """Synchronize; raise DeviceError if an in-kernel barrier wait timed out."""
     ctx = ctx or default_context()

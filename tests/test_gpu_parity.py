@@ -527,3 +527,39 @@ def test_strided_column_slice_encode_decode(torch, rs, rate, N, M, S, cols):
     miss = op == 0
     assert np.array_equal(out[miss][:, a:b], orig[miss][:, a:b])
     assert np.all(out[:, :a] == 0x33) and np.all(out[:, b:] == 0x33)
+
+
+# ---------------------------------------------------------------------------
+# column kernel (one workgroup per pack, 2^7 .. 2^12 rows) vs pass / chain kernels
+
+MONO_CASES = [
+    # encode transform sizes L = 7 .. 12, partial and multi-chunk inputs / outputs
+    ("high", 128, 128, 64), ("high", 200, 256, 64), ("low", 256, 200, 128), ("high", 512, 300, 576),
+    ("default", 1024, 1024, 1024), ("high", 3000, 1024, 64), ("low", 1000, 2500, 128), ("high", 2048, 2048, 64),
+    ("low", 2048, 4000, 64), ("high", 4096, 4096, 64), ("low", 3000, 5000, 64), ("high", 40, 100, 192),
+    ("high", 64, 64, 2048), ("low", 100, 37, 192),
+]
+
+
+@pytest.mark.parametrize("mono", [1, 2, 0])
+@pytest.mark.parametrize("rate,N,M,S", MONO_CASES)
+def test_column_kernel_and_pass_paths_match_oracle(torch, rs, rate, N, M, S, mono):
+    rs.mono_enable(mono)
+    try:
+        orig = O.generate_original(N, S, (N * 3 + M + S) & 0xFF)
+        want = O.encode(rate, orig, M)
+        got = gpu_encode(torch, rs, rate, orig, M)
+        assert np.array_equal(got, want)
+        rng = np.random.default_rng(N * 5 + M)
+        for L in sorted({1, min(N, M) // 3 + 1, min(N, M)}):
+            op = np.ones(N, np.uint8)
+            op[rng.choice(N, L, replace=False)] = 0
+            rp = np.zeros(M, np.uint8)
+            rp[rng.choice(M, L, replace=False)] = 1
+            dw = O.decode(rate, orig, op, want, rp)
+            dg = gpu_decode(torch, rs, rate, orig, op, want, rp)
+            miss = op == 0
+            assert np.array_equal(dg[miss], orig[miss]) and np.array_equal(dg[miss], dw[miss])
+            assert np.all(dg[~miss] == 0x33), "present rows of the output must not be written"
+    finally:
+        rs.mono_enable(1)

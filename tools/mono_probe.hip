@@ -1,0 +1,92 @@
+// Column-kernel timing (development tool): headline encode (1024:1024 x 1 KiB,
+// high rate) through k_mono, back-to-back launch time and per-workgroup
+// s_memrealtime stamps (each stamp first waits for the wave's memory ops).
+// Build: make -C tools _build/mono_probe   Run: tools/_build/mono_probe [n] [S]
+#ifndef RS_MONO_NO_STAMPS
+#define RS_MONO_STAMPS 1
+#endif
+#include "../reed-solomon-simd_amd/csrc/rs_mono.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../reed-solomon-simd_amd/csrc/gf_tables.hpp"
+
+#define CK(x)                                                                        \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                                 \
+        }                                                                            \
+    } while (0)
+
+int main(int argc, char **argv) {
+    const uint32_t n = argc > 1 ? atoi(argv[1]) : 1024, S = argc > 2 ? atoi(argv[2]) : 1024;
+    uint32_t L = 0;
+    while ((1u << L) < n) ++L;
+    const auto &T = rs::tables();
+    const uint32_t nimg = 65536u / n;
+    const size_t words = size_t(n - 1) * rs::kPermWords;
+    std::vector<uint32_t> h(words * nimg);
+    for (uint32_t t = 0; t < nimg; ++t)
+        for (uint32_t b = 0; b < L; ++b)
+            for (uint32_t g = 0; g < (n >> (b + 1)); ++g) {
+                const uint32_t slot = n - (n >> b) + g, idx = (g << (b + 1)) + (1u << b) + t * n - 1;
+                std::copy_n(&T.perm_by_skew[size_t(idx) * rs::kPermWords], rs::kPermWords,
+                            &h[t * words + size_t(slot) * rs::kPermWords]);
+            }
+    uint32_t *d_img;
+    CK(hipMalloc(&d_img, h.size() * 4));
+    CK(hipMemcpy(d_img, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    uint8_t *orig, *rec;
+    CK(hipMalloc(&orig, size_t(n) * S));
+    CK(hipMalloc(&rec, size_t(n) * S));
+    CK(hipMemset(orig, 0x37, size_t(n) * S));
+    rs::MonoArgs A;
+    A.packs = S / 8;
+    A.packs_per_xcd = (A.packs + 7) / 8;
+    A.src[0] = rs::RowMap{orig, S, 0, n};
+    A.nsrc = 1;
+    A.dst = rs::RowMap{rec, S, 0, n};
+    A.chunks = 1;
+    A.img = d_img;
+    A.img_words = words;
+    A.ifft_img = 1;
+    A.fft_img = 0;
+    const int iters = 1000;
+    auto go = [&] { CK(rs::launch_mono(rs::kMonoEncodeHigh, int(L), A, 0)); };
+    for (int i = 0; i < 20; ++i) go();
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < iters; ++i) go();
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    printf("mono encode n=%u S=%u: %.2f us/launch (back-to-back)\n", n, S, ms * 1000 / iters);
+#ifdef RS_MONO_STAMPS
+    CK(hipDeviceSynchronize());
+    go();
+    CK(hipDeviceSynchronize());
+    const uint32_t wgs = 8 * A.packs_per_xcd;
+    std::vector<uint64_t> st(4096 * 16);
+    CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(rs::g_mono_stamps), st.size() * 8));
+    uint64_t t0 = ~0ull;
+    for (uint32_t w = 0; w < wgs; ++w) t0 = std::min(t0, st[w * 16]);
+    const char *names[16] = {"start", "loaded", "", "ifft A done", "remap1 done", "ifft B done", "", "",
+                             "fft B done", "remap2 done", "fft C done", "stored"};
+    const int order[] = {0, 1, 3, 4, 5, 8, 9, 10, 11};
+    for (int i : order) {
+        std::vector<double> v;
+        for (uint32_t w = 0; w < wgs; ++w) v.push_back((st[w * 16 + i] - t0) * 0.01);
+        std::sort(v.begin(), v.end());
+        printf("%-12s min %6.2f  med %6.2f  max %6.2f us\n", names[i], v.front(), v[v.size() / 2], v.back());
+    }
+#endif
+    return 0;
+}
