@@ -142,7 +142,7 @@ def main():
     dom_avg_s = agg[dom][0] / agg[dom][1] / 1e3
     # Algorithmic bytes: an encode must read N*S original
     # bytes and write M*S recovery bytes.  When one launch does the whole
-    # encode (the headline's chain kernel) that is its per-launch figure;
+    # encode (the headline's column kernel) that is its per-launch figure;
     # otherwise the step's algorithmic bytes are priced against the summed
     # duration of all the step's launches.
     alg_step = (N + M) * S

@@ -200,21 +200,17 @@ rs_status rs_engine_formal_derivative(rs_context *ctx, void *d_rows, uint64_t sh
 rs_status rs_profile_enable(rs_context *ctx, int enable);
 int rs_profile_collect(rs_context *ctx, float *ms, uint64_t *bytes, const char **names, int max);
 
-/* ---- chain kernel control (engine tuning, not a reference item) ----
- * Small 2-level transforms run their three passes in one launch whose
- * workgroups meet at in-kernel barriers (DESIGN.md "Chain kernel").
- * rs_chain_enable(ctx, 0) forces one launch per pass (also: environment
- * RS_MI355X_NO_CHAIN=1 at context creation).  rs_check_device synchronizes
- * the device and returns RS_ERR_DEVICE if an in-kernel barrier wait timed out
- * (results of that launch are invalid) since the last check, else RS_OK. */
-rs_status rs_chain_enable(rs_context *ctx, int enable);
+/* ---- device check ----
+ * rs_check_device synchronizes the context's device and returns
+ * RS_ERR_DEVICE (message in rs_last_device_error) if an earlier asynchronous
+ * launch failed, else RS_OK. */
 rs_status rs_check_device(rs_context *ctx);
 
 /* ---- column kernel control (engine tuning, not a reference item) ----
- * Transforms of 2^7 .. 2^12 rows over at most RS_MI355X_MONO_MAX_PACKS (4096)
+ * Transforms of 2^7 .. 2^12 rows over at most RS_MI355X_MONO_MAX_PACKS (256)
  * packs of 4 elements run as one launch in which a workgroup owns every row
  * of one pack (DESIGN.md "Column kernel").  rs_mono_enable(ctx, 0) selects
- * the pass / chain kernels instead (also: RS_MI355X_NO_MONO=1 at context
+ * the pass kernels instead (also: RS_MI355X_NO_MONO=1 at context
  * creation); 1 (default) uses it where it is fastest (single-chunk transforms
  * of 2^7 .. 2^10 rows, twiddles staged in LDS); 2 also for multi-chunk and
  * 2^11 / 2^12-row transforms (also: RS_MI355X_MONO_ALL=1). */

@@ -111,13 +111,6 @@ struct Workspace {
 
 }  // namespace
 
-// Chain kernel limits (DESIGN.md "Chain kernel"): every workgroup of a chain
-// launch must be resident at once, so the grid stays far below capacity.
-constexpr uint32_t kChainMaxSlices = 1024;
-constexpr uint32_t kChainMaxGroups = 1024;         // workgroups per launch
-constexpr uint64_t kChainMaxThreads = 1u << 18;    // 4 waves per SIMD
-constexpr uint64_t kChainMaxBytes = 8ull << 20;    // rows x shard bytes of one transform
-
 // ---------------------------------------------------------------------------
 struct rs_context {
     int device = 0;
@@ -125,12 +118,9 @@ struct rs_context {
     uint32_t *d_lut = nullptr;
     uint16_t *d_lwfold = nullptr;
     uint16_t lw0 = 0;
-    uint32_t *d_sync = nullptr;   // chain-kernel barrier counters (kChainMaxSlices x 32 words)
-    uint32_t *d_fault = nullptr;  // set by a chain kernel whose barrier wait gave up
-    bool chain = true;            // RS_MI355X_NO_CHAIN=1 disables the chain kernel
     bool mono = true;             // RS_MI355X_NO_MONO=1 disables the column kernel
     bool mono_all = false;        // RS_MI355X_MONO_ALL=1: unstaged column kernel too (see use_mono)
-    uint32_t mono_max_packs = 4096;  // column kernel only up to this many packs (RS_MI355X_MONO_MAX_PACKS)
+    uint32_t mono_max_packs = 256;   // column kernel only up to this many packs (RS_MI355X_MONO_MAX_PACKS)
     std::mutex img_mu;            // guards d_img
     uint32_t *d_img[13] = {};     // column-kernel twiddle images per L (built on first use)
     std::mutex mu;  // guards ws (device-resident API scratch)
@@ -260,58 +250,6 @@ void run_level(rs::PassArgs A, const Levels &lv, uint32_t k, int flags, uint32_t
     launch(lv.K[k], flags, A, n >> lv.K[k], lv.lo[k], s, dec_rd, dec_wr);
 }
 
-// Run the three passes of a 2-level transform (level 0 / fused top / level 0)
-// as one chain launch when the matrix is small enough for every workgroup to
-// be resident.  P[k] carry everything but the level geometry; items0 / items2
-// (grid_chunks) count the chunks phases 0 / 2 run over.  Returns false to
-// fall back to three pass launches.
-bool run_chain(rs_context *ctx, int mode, const Levels &lv, const rs::PassArgs P[3], hipStream_t s,
-               uint64_t dec_rd = 0, uint64_t dec_wr = 0) {
-    if (!ctx->chain || lv.m != 2) return false;
-    const uint32_t n = P[0].n, K0 = lv.K[0], K1 = lv.K[1];
-    const uint32_t chunks0 = P[0].grid_chunks, chunks2 = P[2].grid_chunks;
-    if (uint64_t(n) * P[0].packs * 8 > kChainMaxBytes) return false;
-    const uint32_t items[3] = {(n >> K0) * chunks0, n >> K1, (n >> K0) * chunks2};
-    const uint32_t most = std::max(items[0], std::max(items[1], items[2]));
-    for (int spl = 4; spl <= 6; ++spl) {
-        const uint32_t slices = (P[0].packs + (1u << spl) - 1) >> spl;
-        if (slices > kChainMaxSlices) continue;
-        const int gb = rs::chain_gb(int(K1), spl);
-        // one block per workgroup and phase (the chain stages all tables up front)
-        const uint32_t members = most;
-        if (uint64_t(slices) * members > kChainMaxGroups) continue;
-        if ((uint64_t(slices) * members << (gb + spl)) > kChainMaxThreads) continue;
-        rs::ChainArgs C;
-        for (int k = 0; k < 3; ++k) {
-            C.ph[k] = P[k];
-            C.ph[k].slices = slices;
-            C.ph[k].nsets = n >> lv.K[k == 1 ? 1 : 0];
-            C.ph[k].a = lv.lo[k == 1 ? 1 : 0];
-            C.items[k] = items[k];
-        }
-        C.members = members;
-        C.sync = ctx->d_sync;
-        C.fault = ctx->d_fault;
-        hipEvent_t ev = nullptr;
-        if (t_prof_ctx) prof_begin(s, &ev);
-        const hipError_t e = rs::launch_chain(mode, int(K0), int(K1), spl, C, s);
-        if (e == hipErrorNotSupported) return false;
-        check(e);
-        if (t_prof_ctx) {
-            // same spelling as the rocprofv3 kernel trace (template arguments)
-            static thread_local char buf[64];
-            snprintf(buf, sizeof buf, "k_chain<%u, %u, %d, %d>", K0, K1, spl, mode);
-            // algorithmic bytes: the three passes' reads + writes
-            uint64_t bytes = 0;
-            for (int k = 0; k < 3; ++k)
-                bytes += pass_bytes(int(lv.K[k == 1 ? 1 : 0]), C.ph[k], k == 0 ? dec_rd : 0, k == 2 ? dec_wr : 0);
-            prof_end(s, ev, buf, bytes);
-        }
-        return true;
-    }
-    return false;
-}
-
 // Column kernel (rs_mono.hip): twiddle images of a 2^L-row transform for
 // every skew offset t * n, t = 0 .. 65536/n - 1 (rs_device.hpp), built on the
 // host from the skew tables once per context and L.
@@ -340,7 +278,7 @@ const uint32_t *mono_images(rs_context *ctx, uint32_t L) {
     return d;
 }
 
-// The column kernel runs where it beats the pass / chain kernels: its staged
+// The column kernel runs where it beats the pass kernels: its staged
 // variant (one chunk, L <= 10).  RS_MI355X_MONO_ALL=1 also routes multi-chunk
 // and L = 11, 12 transforms to its unstaged variant (tests, tuning).
 bool use_mono(rs_context *ctx, uint32_t L, const Geom &g, uint32_t chunks) {
@@ -404,13 +342,6 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
     }
     uint8_t *W = static_cast<uint8_t *>(ws.buf[0].get(size_t(C) * n * g.stride));
     A.work_stride = g.stride;
-    if (lv.m == 2) {
-        rs::PassArgs P[3] = {A, A, A};
-        P[0].grid_chunks = C, P[0].src[0] = src, P[0].nsrc = 1, P[0].work_out = W;
-        P[1].work_in = W, P[1].in_chunks = C, P[1].work_out = W;
-        P[2].work_in = W, P[2].dst = dst;
-        if (run_chain(ctx, rs::kChainEncodeHigh, lv, P, s)) return;
-    }
     for (uint32_t k = 0; k + 1 < lv.m; ++k) {  // IFFT, low levels, every chunk
         rs::PassArgs P = A;
         P.grid_chunks = C;
@@ -467,13 +398,6 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
     uint8_t *W = static_cast<uint8_t *>(ws.buf[0].get(size_t(n) * g.stride));
     uint8_t *W2 = static_cast<uint8_t *>(ws.buf[1].get(size_t(C) * n * g.stride));
     A.work_stride = g.stride;
-    if (lv.m == 2) {
-        rs::PassArgs P[3] = {A, A, A};
-        P[0].src[0] = src, P[0].nsrc = 1, P[0].work_out = W;
-        P[1].work_in = W, P[1].out_chunks = C, P[1].work_out = W2;
-        P[2].grid_chunks = C, P[2].work_in = W2, P[2].dst = dst;
-        if (run_chain(ctx, rs::kChainEncodeLow, lv, P, s)) return;
-    }
     for (uint32_t k = 0; k + 1 < lv.m; ++k) {
         rs::PassArgs P = A;
         if (k == 0) P.src[0] = src, P.nsrc = 1;
@@ -523,12 +447,28 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
     uint64_t received = 0, missing = 0;
     for (uint32_t r = 0; r < nd; ++r) received += st[r] == 2;
     for (uint64_t i = 0; i < N; ++i) missing += !orig_present[i];
-    uint8_t *d_state = static_cast<uint8_t *>(ws.state.get(nd));
     uint32_t *d_rowinfo = static_cast<uint32_t *>(ws.rowinfo.get(size_t(nd) * 4));
-    check(hipMemcpyAsync(d_state, st.data(), nd, hipMemcpyHostToDevice, s));
+    rs::EvalArgs E;
+    E.u = u;
+    E.low_rate = high ? 0 : 1;
+    E.end = end;
+    E.lw0 = ctx->lw0;
+    E.lw_fold = ctx->d_lwfold + (nd - 1);
+    E.rowinfo = d_rowinfo;
+    if (nd <= rs::kEvalInlineRows) {
+        // the erasure state rides in the kernel arguments: no copy
+        for (uint32_t r = 0; r < nd; ++r) {
+            E.erased[r >> 5] |= uint32_t(st[r] == 1) << (r & 31);
+            E.received[r >> 5] |= uint32_t(st[r] == 2) << (r & 31);
+        }
+    } else {
+        uint8_t *d_state = static_cast<uint8_t *>(ws.state.get(nd));
+        check(hipMemcpyAsync(d_state, st.data(), nd, hipMemcpyHostToDevice, s));
+        E.state = d_state;
+    }
     hipEvent_t ev = nullptr;
     if (t_prof_ctx) prof_begin(s, &ev);
-    check(rs::launch_eval_poly(u, !high, end, d_state, ctx->d_lwfold + (nd - 1), ctx->lw0, d_rowinfo, s));
+    check(rs::launch_eval_poly(E, s));
     if (t_prof_ctx) prof_end(s, ev, "k_eval_poly", uint64_t(nd) * 5);
 
     rs::PassArgs A = base_args(ctx, g, nd);
@@ -562,13 +502,6 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
     for (uint32_t k = 0; k + 1 < lv.m; ++k) X[k] = static_cast<uint8_t *>(ws.buf[k].get(size_t(nd) * g.stride));
     uint8_t *U = static_cast<uint8_t *>(ws.buf[3].get(size_t(nd) * g.stride));
     A.work_stride = g.stride;
-    if (lv.m == 2) {
-        rs::PassArgs P[3] = {A, A, A};
-        P[0].src[0] = rec_map, P[0].src[1] = orig_map, P[0].nsrc = 2, P[0].load_scale = 1, P[0].work_out = X[0];
-        P[1].work_in = X[0], P[1].fd_mode = 1, P[1].work_out = U;
-        P[2].work_in = X[0], P[2].fd_mode = 2, P[2].xor_in = U, P[2].dst = out_map, P[2].reveal = 1;
-        if (run_chain(ctx, rs::kChainDecode, lv, P, s, received, missing)) return;
-    }
     for (uint32_t k = 0; k + 1 < lv.m; ++k) {  // scale received rows (level 0), IFFT low levels
         rs::PassArgs P = A;
         if (k == 0) {
@@ -733,12 +666,6 @@ rs_status rs_context_create(int device, rs_context **out) {
         check(hipMemcpy(ctx->d_lut, T.perm_by_log.data(), T.perm_by_log.size() * 4, hipMemcpyHostToDevice));
         check(hipMemcpy(ctx->d_lwfold, T.lw_fold.data(), T.lw_fold.size() * 2, hipMemcpyHostToDevice));
         ctx->lw0 = T.log_walsh[0];
-        check(hipMalloc(&ctx->d_sync, size_t(kChainMaxSlices) * 32 * 4));
-        check(hipMemset(ctx->d_sync, 0, size_t(kChainMaxSlices) * 32 * 4));
-        check(hipMalloc(&ctx->d_fault, 4));
-        check(hipMemset(ctx->d_fault, 0, 4));
-        const char *nc = getenv("RS_MI355X_NO_CHAIN");
-        ctx->chain = !(nc && nc[0] == '1');
         const char *nm = getenv("RS_MI355X_NO_MONO");
         ctx->mono = !(nm && nm[0] == '1');
         const char *ma = getenv("RS_MI355X_MONO_ALL");
@@ -759,10 +686,8 @@ void rs_context_destroy(rs_context *ctx) {
     if (ctx->d_tw) (void)hipFree(ctx->d_tw);
     if (ctx->d_lut) (void)hipFree(ctx->d_lut);
     if (ctx->d_lwfold) (void)hipFree(ctx->d_lwfold);
-    if (ctx->d_sync) (void)hipFree(ctx->d_sync);
     for (uint32_t *p : ctx->d_img)
         if (p) (void)hipFree(p);
-    if (ctx->d_fault) (void)hipFree(ctx->d_fault);
     delete ctx;
 }
 
@@ -1186,13 +1111,6 @@ rs_status rs_profile_enable(rs_context *ctx, int enable) {
     return RS_OK;
 }
 
-rs_status rs_chain_enable(rs_context *ctx, int enable) {
-    if (!ctx) return RS_ERR_INVALID_ARGUMENT;
-    std::lock_guard<std::mutex> lock(ctx->mu);
-    ctx->chain = enable != 0;
-    return RS_OK;
-}
-
 rs_status rs_mono_enable(rs_context *ctx, int enable) {
     if (!ctx) return RS_ERR_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> lock(ctx->mu);
@@ -1206,13 +1124,7 @@ rs_status rs_check_device(rs_context *ctx) {
     return guarded(nullptr, [&]() -> rs_status {
         check(hipSetDevice(ctx->device));
         check(hipDeviceSynchronize());
-        uint32_t fault = 0;
-        check(hipMemcpy(&fault, ctx->d_fault, 4, hipMemcpyDeviceToHost));
-        if (fault) {
-            check(hipMemset(ctx->d_fault, 0, 4));
-            g_last_error = "chain kernel: in-kernel barrier wait timed out";
-            return RS_ERR_DEVICE;
-        }
+        check(hipGetLastError());
         return RS_OK;
     });
 }

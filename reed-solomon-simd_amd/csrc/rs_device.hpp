@@ -69,37 +69,6 @@ enum PassFlags {
 // Launch one pass on `stream`.  K = log2(rows per set).
 hipError_t launch_pass(int K, int flags, const PassArgs &args, hipStream_t stream);
 
-// Three passes of a 2-level transform in one launch (DESIGN.md "Chain
-// kernel"): phase 0 = level 0 (K0 bits), phase 1 = fused top level (K1 bits),
-// phase 2 = level 0 again.  Every PassArgs has the same `slices` (packs per
-// slice 2^spl); the grid is slices x members workgroups and member q runs
-// blocks q, q + members, ... of each phase's items (set + chunk * nsets).
-enum ChainMode { kChainEncodeHigh = 0, kChainEncodeLow = 1, kChainDecode = 2 };
-// Rows per lane (log2) in the chain's smaller level; workgroups are
-// 2^(K1 - kChainLR) row groups x 2^spl packs (at most 1024 threads).
-#ifndef RS_CHAIN_LR
-#define RS_CHAIN_LR 1
-#endif
-constexpr int kChainLR = RS_CHAIN_LR;
-// log2 row groups of a chain workgroup: at least one wave (2^(gb+spl) >= 64),
-// at most 1024 threads, at least one row per lane in the smaller level.
-constexpr int chain_gb(int K1, int spl) {
-    int gb = K1 - kChainLR;
-    if (gb < 6 - spl) gb = 6 - spl;
-    if (gb > 10 - spl) gb = 10 - spl;
-    if (gb > K1 - 1) gb = K1 - 1;
-    return gb;
-}
-struct ChainArgs {
-    PassArgs ph[3];
-    uint32_t items[3] = {0, 0, 0};
-    uint32_t members = 0;
-    uint32_t *sync = nullptr;   // 32 words per slice, zero between launches
-    uint32_t *fault = nullptr;  // set if a barrier wait gave up
-};
-// hipErrorNotSupported: no chain kernel for this (K0, K1, spl).
-hipError_t launch_chain(int mode, int K0, int K1, int spl, const ChainArgs &C, hipStream_t stream);
-
 // Column kernel (DESIGN.md "Column kernel"): one workgroup owns ALL n = 2^L
 // transform rows of one pack (4 elements of every row), so a whole encode or
 // decode runs without any cross-workgroup exchange.  Twiddles come from
@@ -127,13 +96,24 @@ hipError_t launch_mono(int mode, int L, const MonoArgs &A, hipStream_t stream);
 bool mono_staged(int L, uint32_t chunks);
 int mono_rows_log2_per_lane(int L);
 
-// eval_poly for a decode: erasure vector -> per-row log factors.
-//   state[r] (r < 2^u): bit0 = erasure-vector entry, bit1 = row received.
+// eval_poly for a decode (src/engine/utils.rs:20-31) reduced to 2^u points
+// (DESIGN.md "eval_poly"): erasure vector -> per-row log factors.
+//   row r < 2^u: erased bit e(r) (erasure-vector entry) and received bit.
 //   low_rate: the erasure vector is also 1 on [2^u, 65536) (rate_low.rs:196).
-//   end: recovery_end / original_end (rows >= end are zero in the vector for high rate).
-hipError_t launch_eval_poly(uint32_t u, bool low_rate, uint32_t end, const uint8_t *state,
-                            const uint16_t *lw_fold_u, uint16_t log_walsh0, uint32_t *rowinfo,
-                            hipStream_t stream);
+//   end: recovery_end / original_end.
+// Output rowinfo[r] = log factor | (received ? 0 : 0x10000).
+// Rows' bits travel in the kernel arguments when 2^u <= kEvalInlineRows (no
+// copy, no extra launch), else in a device byte array (bit0 erased, bit1 received).
+constexpr uint32_t kEvalInlineRows = 8192;
+struct EvalArgs {
+    uint32_t u = 0, low_rate = 0, end = 0, lw0 = 0;
+    const uint16_t *lw_fold = nullptr;  // lw_fold for this u (2^u entries)
+    uint32_t *rowinfo = nullptr;
+    const uint8_t *state = nullptr;     // 2^u > kEvalInlineRows only
+    uint32_t erased[kEvalInlineRows / 32] = {};
+    uint32_t received[kEvalInlineRows / 32] = {};
+};
+hipError_t launch_eval_poly(const EvalArgs &A, hipStream_t stream);
 
 // x[rows] *= exp(log_m) over `blocks` 64-byte blocks.
 hipError_t launch_mul(uint8_t *rows, uint64_t blocks, const uint32_t *lut_entry, hipStream_t stream);

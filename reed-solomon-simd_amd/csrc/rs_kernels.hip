@@ -23,13 +23,6 @@
 namespace rs {
 namespace {
 
-#ifdef RS_CHAIN_STAMPS  // tools/chain_probe.hip: per-workgroup timestamps
-__device__ uint64_t g_chain_stamps[4096][32];
-#define RS_STAMP(i) \
-    if (threadIdx.x == 0 && blockIdx.x < 4096) g_chain_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime()
-#else
-#define RS_STAMP(i)
-#endif
 
 // -------------------------------------------------------------------------
 // Pass kernel.
@@ -55,7 +48,7 @@ struct Pass {
     // Left alone, the compiler interleaves every butterfly of a layer and
     // hoists all their tables: with 8 rows per lane that costs occupancy or
     // spills, so wide shapes run one table / butterfly at a time per wave.
-    static constexpr bool kChain = R >= 8;
+    static constexpr bool kSerial = R >= 8;
     static_assert(K == 0 || (LR >= 1 && LR <= K), "register bits must fit the set");
     static_assert(kThreads >= 64, "at least one full wave");
 
@@ -95,24 +88,9 @@ __device__ __forceinline__ uint32_t pin(uint32_t r) {
     return r;
 }
 
-// Row words of the work buffers.  COH: write-through / coherent accesses
-// (agent-scope relaxed atomics: global_load/store sc1) for rows handed
-// between workgroups inside one launch (k_chain, DESIGN.md "Chain kernel").
-template <bool COH>
-__device__ __forceinline__ uint32_t ld32(const uint8_t *p) {
-    if constexpr (COH)
-        return __hip_atomic_load(reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(p)), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-    else
-        return *reinterpret_cast<const uint32_t *>(p);
-}
-template <bool COH>
-__device__ __forceinline__ void st32(uint8_t *p, uint32_t v) {
-    if constexpr (COH)
-        __hip_atomic_store(reinterpret_cast<uint32_t *>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        *reinterpret_cast<uint32_t *>(p) = v;
-}
+// Row words of the work buffers.
+__device__ __forceinline__ uint32_t ld32(const uint8_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
+__device__ __forceinline__ void st32(uint8_t *p, uint32_t v) { *reinterpret_cast<uint32_t *>(p) = v; }
 
 // LDS layout (dynamic, 16-byte aligned), in 32-bit words:
 //   planes : 2 x (2^K rows x SP packs): low and high words of the exchange
@@ -250,7 +228,7 @@ __device__ __forceinline__ void stage_twiddles(const PassArgs &A, const Ctx &c, 
 // Load the lane's rows (phase PH) of `chunk`.  SCALE: rows erased in the
 // decode's erasure vector load as zero (checked in global rowinfo, so the
 // load need not wait for staging).
-template <int K, int LR, int SPL, int PH, bool SCALE, bool COH = false>
+template <int K, int LR, int SPL, int PH, bool SCALE>
 __device__ __forceinline__ void load_rows(const PassArgs &A, const Ctx &c, uint32_t chunk, uint32_t (&lo)[1 << LR],
                                           uint32_t (&hi)[1 << LR]) {
     using P = Pass<K, LR, SPL>;
@@ -269,8 +247,8 @@ __device__ __forceinline__ void load_rows(const PassArgs &A, const Ctx &c, uint3
         if (SCALE && (A.rowinfo[r] & 0x10000u)) p = nullptr;
         uint32_t l = 0, h = 0;
         if (p && c.pk_ok) {
-            l = ld32<COH>(p + c.pk_off);
-            h = ld32<COH>(p + c.pk_off + 32);
+            l = ld32(p + c.pk_off);
+            h = ld32(p + c.pk_off + 32);
         }
         lo[i] = l;
         hi[i] = h;
@@ -285,7 +263,7 @@ __device__ __forceinline__ void scale_rows(const Ctx &c, const uint32_t *tabS, u
     static_for<0, P::R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         uint32_t off = P::template lrow<PH>(c.g, i) * 20u;
-        if constexpr (P::kChain) {
+        if constexpr (P::kSerial) {
             if constexpr (P::kUniform) asm volatile("" : "+s"(off), "+v"(lo[i]), "+v"(hi[i]) : "v"(dep));
             else asm volatile("" : "+v"(off), "+v"(lo[i]), "+v"(hi[i]) : "v"(dep));
         }
@@ -294,7 +272,7 @@ __device__ __forceinline__ void scale_rows(const Ctx &c, const uint32_t *tabS, u
     });
 }
 
-template <int K, int LR, int SPL, int PH, bool REVEAL, bool COH = false>
+template <int K, int LR, int SPL, int PH, bool REVEAL>
 __device__ __forceinline__ void store_rows(const PassArgs &A, const Ctx &c, uint32_t chunk, const uint32_t *tabV,
                                            const uint32_t *rinfo, uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
     using P = Pass<K, LR, SPL>;
@@ -314,8 +292,8 @@ __device__ __forceinline__ void store_rows(const PassArgs &A, const Ctx &c, uint
             }
         }
         if (p && c.pk_ok) {
-            st32<COH>(p + c.pk_off, l);
-            st32<COH>(p + c.pk_off + 32, h);
+            st32(p + c.pk_off, l);
+            st32(p + c.pk_off + 32, h);
         }
     });
 }
@@ -333,7 +311,7 @@ __device__ __forceinline__ void layer(const Ctx &c, const uint32_t *tab, uint32_
     static_for<0, (P::R >> (RB + 1))>([&](auto gc) {
         constexpr int i0 = decltype(gc)::value << (RB + 1);
         uint32_t off = tw_slot<K>(B, P::template lrow<PH>(c.g, i0)) * 20u;
-        if constexpr (P::kChain) {  // one table in flight
+        if constexpr (P::kSerial) {  // one table in flight
             if constexpr (P::kUniform) asm volatile("" : "+s"(off) : "v"(dep));
             else asm volatile("" : "+v"(off) : "v"(dep));
         }
@@ -347,7 +325,7 @@ __device__ __forceinline__ void layer(const Ctx &c, const uint32_t *tab, uint32_
         static_for<0, (1 << RB)>([&](auto lc) {
             constexpr int i = i0 | decltype(lc)::value;
             constexpr int i2 = i | (1 << RB);
-            if constexpr (P::kChain) asm volatile("" : "+v"(lo[i]), "+v"(hi[i]), "+v"(lo[i2]), "+v"(hi[i2]) : "v"(dep));
+            if constexpr (P::kSerial) asm volatile("" : "+v"(lo[i]), "+v"(hi[i]), "+v"(lo[i2]), "+v"(hi[i2]) : "v"(dep));
             if constexpr (IFFT) ifft_bfly(lo[i], hi[i], lo[i2], hi[i2], t);
             else fft_bfly(lo[i], hi[i], lo[i2], hi[i2], t);
             dep = lo[i];
@@ -438,7 +416,7 @@ __device__ __forceinline__ void formal_derivative(const Ctx &c, uint32_t mode, u
     });
 }
 
-template <int K, int LR, int SPL, int PH, bool COH>
+template <int K, int LR, int SPL, int PH>
 __device__ __forceinline__ void load_xor_rows(const PassArgs &A, const Ctx &c, uint32_t (&lo)[1 << LR],
                                               uint32_t (&hi)[1 << LR]) {
     using P = Pass<K, LR, SPL>;
@@ -448,8 +426,8 @@ __device__ __forceinline__ void load_xor_rows(const PassArgs &A, const Ctx &c, u
         const uint8_t *p = A.xor_in + uint64_t(r) * A.work_stride;
         uint32_t l = 0, h = 0;
         if (c.pk_ok) {
-            l = ld32<COH>(p + c.pk_off);
-            h = ld32<COH>(p + c.pk_off + 32);
+            l = ld32(p + c.pk_off);
+            h = ld32(p + c.pk_off + 32);
         }
         lo[i] = l;
         hi[i] = h;
@@ -508,7 +486,7 @@ __device__ __forceinline__ void transform(const Ctx &c, uint32_t *plane, const u
 #ifdef RS_PROBE_SKIP_XFORM  // tools/pass_probe.hip: time a pass without its layers
     return;
 #endif
-    if constexpr (P::kChain || K == 0) {
+    if constexpr (P::kSerial || K == 0) {
         static_for<0, K>([&](auto bc) {
             constexpr int n = decltype(bc)::value;
             constexpr int b = IFFT ? n : K - 1 - n;
@@ -570,20 +548,9 @@ __device__ __forceinline__ Stager<K, Pass<K, LR, SPL>::kThreads> stager_for(uint
     return st;
 }
 
-struct NoExtra {
-    __device__ __forceinline__ void operator()() const {}
-};
-
 // One pass over workgroup-block (bx = set * slices + slice, by = chunk).
-// COH_LD / COH_ST: work-buffer rows are handed between workgroups of one
-// launch (k_chain phases), so they are read / written coherently.
-// STAGED: the block's tables are staged by the caller, whose `extra` runs
-// between the row loads and the barrier (k_chain stages every phase's tables
-// in phase 0's load window).
-template <int K, int LR, int SPL, int FLAGS, bool COH_LD, bool COH_ST, int STAMP = -1, bool STAGED = false,
-          typename Extra = NoExtra>
-__device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32_t by, uint32_t *lds,
-                                          const Extra &extra = Extra()) {
+template <int K, int LR, int SPL, int FLAGS>
+__device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32_t by, uint32_t *lds) {
     using P = Pass<K, LR, SPL>;
     using L = Lds<K, SPL, FLAGS>;
     constexpr bool DO_IFFT = FLAGS & kIfft;
@@ -606,17 +573,14 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
     uint32_t lo[P::R], hi[P::R];
     uint32_t xl[XOR_IN ? P::R : 1], xh[XOR_IN ? P::R : 1];
     // loads first, then table staging: one barrier covers both latencies
-    load_rows<K, LR, SPL, DO_IFFT ? 0 : PL, SCALE, COH_LD>(A, c, gchunk, lo, hi);
-    if constexpr (XOR_IN) load_xor_rows<K, LR, SPL, PL, COH_LD>(A, c, xl, xh);
-    if constexpr (!STAGED) {
+    load_rows<K, LR, SPL, DO_IFFT ? 0 : PL, SCALE>(A, c, gchunk, lo, hi);
+    if constexpr (XOR_IN) load_xor_rows<K, LR, SPL, PL>(A, c, xl, xh);
+    {
         auto st = stager_for<K, LR, SPL, FLAGS>(lds);
         st.load(A, c, gchunk);
         st.store();
-    } else {
-        extra();
     }
     __syncthreads();
-    if constexpr (STAMP >= 0) RS_STAMP(STAMP);
     if constexpr (SCALE) scale_rows<K, LR, SPL, 0>(c, tabS, lo, hi);
 
     if constexpr (DO_IFFT) {
@@ -625,7 +589,7 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
             for (uint32_t ci = 1; ci < A.in_chunks; ++ci) {
                 const uint32_t chunk = gchunk + ci;
                 uint32_t tl[P::R], th[P::R];
-                load_rows<K, LR, SPL, 0, false, COH_LD>(A, c, chunk, tl, th);
+                load_rows<K, LR, SPL, 0, false>(A, c, chunk, tl, th);
                 __syncthreads();
                 if constexpr (K > 0) stage_twiddles<K, P::kThreads>(A, c, chunk, tabI, nullptr);
                 __syncthreads();
@@ -641,8 +605,7 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
 
     if constexpr (DO_FFT && !MULTI_OUT) {
         transform<K, LR, SPL, false>(c, plane, tabF, lo, hi);
-        if constexpr (STAMP >= 0) RS_STAMP(STAMP + 1);
-        store_rows<K, LR, SPL, 0, REVEAL, COH_ST>(A, c, gchunk, tabV, rinfo, lo, hi);
+        store_rows<K, LR, SPL, 0, REVEAL>(A, c, gchunk, tabV, rinfo, lo, hi);
     } else if constexpr (DO_FFT) {
         for (uint32_t co = 0; co < A.out_chunks; ++co) {
             const uint32_t chunk = gchunk + co;
@@ -652,18 +615,17 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
             if constexpr (K > 0) stage_twiddles<K, P::kThreads>(A, c, chunk, nullptr, tabF);
             __syncthreads();
             transform<K, LR, SPL, false>(c, plane, tabF, yl, yh);
-            store_rows<K, LR, SPL, 0, false, COH_ST>(A, c, chunk, tabV, rinfo, yl, yh);
+            store_rows<K, LR, SPL, 0, false>(A, c, chunk, tabV, rinfo, yl, yh);
         }
     } else {
-        if constexpr (STAMP >= 0) RS_STAMP(STAMP + 1);
-        store_rows<K, LR, SPL, PL, REVEAL, COH_ST>(A, c, gchunk, tabV, rinfo, lo, hi);
+        store_rows<K, LR, SPL, PL, REVEAL>(A, c, gchunk, tabV, rinfo, lo, hi);
     }
 }
 
 template <int K, int LR, int SPL, int FLAGS>
 __global__ void __launch_bounds__(1 << (K - LR + SPL), 2) k_pass(const PassArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    pass_body<K, LR, SPL, FLAGS, false, false>(A, blockIdx.x, blockIdx.y, lds);
+    pass_body<K, LR, SPL, FLAGS>(A, blockIdx.x, blockIdx.y, lds);
 }
 
 template <int K, int LR, int SPL, int F>
@@ -728,214 +690,6 @@ hipError_t launch_shape(bool narrow, int flags, const PassArgs &A, hipStream_t s
 }
 
 
-// ---------------------------------------------------------------------------
-// Chain kernel: the three passes of a 2-level transform (level 0, fused top
-// level 1, level 0) in ONE launch.  Columns are independent, so only the
-// workgroups of one column slice exchange rows; they meet at a barrier after
-// phases 0 and 1 (write-through row stores, vmcnt(0), workgroup barrier,
-// one agent-scope counter add per workgroup, a coherent poll; rows are read
-// back coherently).  Launch boundaries cost ~1.5 us of GPU time plus ~2-3 us
-// of host enqueue each; a slice barrier ~1 us.  All workgroups must be
-// co-resident: the host sizes the grid far below capacity, and every wait is
-// bounded (a timed-out wait sets *fault instead of hanging the device).
-constexpr uint32_t kSpinLimit = 1u << 21;
-
-// `during` runs on every thread between this workgroup's arrival and the
-// wait (loads issued there overlap the barrier).
-template <typename During = NoExtra>
-__device__ __forceinline__ void slice_barrier(uint32_t *ctr, uint32_t members, uint32_t *fault,
-                                              const During &during = During()) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    during();
-    if (threadIdx.x == 0) {
-        uint32_t spins = 0;
-        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < members) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > kSpinLimit) {
-                __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-    }
-    __syncthreads();
-}
-
-template <int MODE>
-struct ChainFlags;
-template <>
-struct ChainFlags<kChainEncodeHigh> {
-    static constexpr int F0 = kIfft, F1 = kIfft | kFft | kMultiIn, F2 = kFft;
-};
-template <>
-struct ChainFlags<kChainEncodeLow> {
-    static constexpr int F0 = kIfft, F1 = kIfft | kFft | kMultiOut, F2 = kFft;
-};
-template <>
-struct ChainFlags<kChainDecode> {
-    static constexpr int F0 = kIfft | kScale, F1 = kIfft | kFft | kFd, F2 = kFft | kFd | kXorIn | kReveal;
-};
-
-// LDS words of a phase region (16-byte aligned)
-template <int K, int SPL, int FLAGS>
-constexpr uint32_t chain_region() {
-    return (Lds<K, SPL, FLAGS>::words + 3u) & ~3u;
-}
-
-template <int K0, int K1, int SPL, int MODE>
-__global__ void __launch_bounds__(1 << (chain_gb(K1, SPL) + SPL)) k_chain(const ChainArgs C) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    constexpr int GB = chain_gb(K1, SPL);
-    constexpr int LR0 = K0 - GB, LR1 = K1 - GB;
-    using Fl = ChainFlags<MODE>;
-    // every phase's tables stay resident: one staging round trip for all three
-    uint32_t *lds0 = lds;
-    uint32_t *lds1 = lds0 + chain_region<K0, SPL, Fl::F0>();
-    uint32_t *lds2 = lds1 + chain_region<K1, SPL, Fl::F1>();
-    const uint32_t nsl = C.ph[0].slices;
-    const uint32_t slice = blockIdx.x % nsl, q = blockIdx.x / nsl;
-    uint32_t *ctr = C.sync + slice * 32u;
-    RS_STAMP(0);
-    // Workgroup q runs item q of each phase (the host guarantees items[p] <=
-    // members): set q % nsets, chunk q / nsets.
-    uint32_t bx[3], by[3];
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-        bx[p] = (q % C.ph[p].nsets) * nsl + slice;
-        by[p] = q / C.ph[p].nsets;
-    }
-    // Table staging off the critical path: phase 0's tables load beside its
-    // row loads; phase 1's and 2's load while the workgroup waits at the
-    // preceding slice barrier, and land in LDS right after it.
-    const bool a0 = q < C.items[0], a1 = q < C.items[1], a2 = q < C.items[2];
-    auto s0 = stager_for<K0, LR0, SPL, Fl::F0>(lds0);
-    auto s1 = stager_for<K1, LR1, SPL, Fl::F1>(lds1);
-    auto s2 = stager_for<K0, LR0, SPL, Fl::F2>(lds2);
-    if (a0) {
-        pass_body<K0, LR0, SPL, Fl::F0, false, true, 8, true>(C.ph[0], bx[0], by[0], lds0, [&]() {
-            s0.load(C.ph[0], make_ctx<K0, LR0, SPL>(C.ph[0], bx[0]), by[0]);
-            s0.store();
-        });
-    }
-    RS_STAMP(1);
-    slice_barrier(ctr, C.members, C.fault, [&]() {
-        if (a1) s1.load(C.ph[1], make_ctx<K1, LR1, SPL>(C.ph[1], bx[1]), by[1]);
-    });
-    if (a1) s1.store();
-    RS_STAMP(2);
-    if (a1) pass_body<K1, LR1, SPL, Fl::F1, true, true, 10, true>(C.ph[1], bx[1], by[1], lds1);
-    RS_STAMP(3);
-    slice_barrier(ctr + 1, C.members, C.fault, [&]() {
-        if (a2) s2.load(C.ph[2], make_ctx<K0, LR0, SPL>(C.ph[2], bx[2]), by[2]);
-    });
-    if (a2) s2.store();
-    RS_STAMP(4);
-    if (a2) pass_body<K0, LR0, SPL, Fl::F2, true, false, 12, true>(C.ph[2], bx[2], by[2], lds2);
-    RS_STAMP(5);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    RS_STAMP(6);
-    // Leave the counters zero for the next launch: the last workgroup out
-    // (every member has passed both waits) resets them.
-    if (threadIdx.x == 0) {
-        const uint32_t out = __hip_atomic_fetch_add(ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (out == C.members - 1) {
-            __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(ctr + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-template <int K0, int K1, int SPL, int MODE>
-hipError_t launch_chain_f(const ChainArgs &C, hipStream_t s) {
-    constexpr int GB = chain_gb(K1, SPL);
-    using Fl = ChainFlags<MODE>;
-    constexpr size_t lds = size_t(chain_region<K0, SPL, Fl::F0>() + chain_region<K1, SPL, Fl::F1>() +
-                                  chain_region<K0, SPL, Fl::F2>()) * 4;
-    static bool attr_set = false;
-    if (!attr_set && lds > 65536) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_chain<K0, K1, SPL, MODE>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
-    k_chain<K0, K1, SPL, MODE><<<dim3(C.ph[0].slices * C.members), 1 << (GB + SPL), lds, s>>>(C);
-    return hipGetLastError();
-}
-
-template <int K0, int K1, int MODE>
-hipError_t launch_chain_s(int spl, const ChainArgs &C, hipStream_t s) {
-    switch (spl) {
-        case 4: return launch_chain_f<K0, K1, 4, MODE>(C, s);
-        case 5: return launch_chain_f<K0, K1, 5, MODE>(C, s);
-        case 6: return launch_chain_f<K0, K1, 6, MODE>(C, s);
-        default: return hipErrorNotSupported;
-    }
-}
-
-template <int MODE>
-hipError_t launch_chain_m(int K0, int K1, int spl, const ChainArgs &C, hipStream_t s) {
-    switch (K0 * 8 + K1) {
-        case 4 * 8 + 3: return launch_chain_s<4, 3, MODE>(spl, C, s);
-        case 4 * 8 + 4: return launch_chain_s<4, 4, MODE>(spl, C, s);
-        case 5 * 8 + 4: return launch_chain_s<5, 4, MODE>(spl, C, s);
-        case 5 * 8 + 5: return launch_chain_s<5, 5, MODE>(spl, C, s);
-        case 6 * 8 + 5: return launch_chain_s<6, 5, MODE>(spl, C, s);
-        case 6 * 8 + 6: return launch_chain_s<6, 6, MODE>(spl, C, s);
-        default: return hipErrorNotSupported;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// eval_poly (reference src/engine/utils.rs:20-31) reduced to 2^u points:
-// the erasure vector is zero outside [0, 2^u) (high rate) or equals 1 there
-// (low rate), so FWHT_16 collapses onto 2^u residues (DESIGN.md "eval_poly").
-__device__ __forceinline__ uint32_t add_mod(uint32_t a, uint32_t b) {
-    const uint32_t s = a + b;
-    return (s + (s >> 16)) & 0xFFFFu;
-}
-__device__ __forceinline__ uint32_t sub_mod(uint32_t a, uint32_t b) {
-    const uint32_t d = a - b;
-    return (d + (d >> 16)) & 0xFFFFu;
-}
-
-__device__ void walsh_lds(uint16_t *v, uint32_t u) {
-    const uint32_t n = 1u << u;
-    for (uint32_t h = 1; h < n; h <<= 1) {
-        for (uint32_t k = threadIdx.x; k < n / 2; k += blockDim.x) {
-            const uint32_t i = (k / h) * 2 * h + (k % h);
-            const uint32_t p = v[i], q = v[i + h];
-            v[i] = add_mod(p, q);
-            v[i + h] = sub_mod(p, q);
-        }
-        __syncthreads();
-    }
-}
-
-__global__ void __launch_bounds__(1024) k_eval_poly(uint32_t u, uint32_t low_rate, uint32_t end, const uint8_t *state,
-                                                    const uint16_t *lw_fold, uint32_t lw0, uint32_t *rowinfo) {
-    extern __shared__ __attribute__((aligned(16))) uint16_t v[];
-    const uint32_t n = 1u << u;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint32_t e = state[i] & 1u;
-        // high rate: v = e;  low rate: v = e - 1 on [0, end), 0 beyond  (mod 65535)
-        v[i] = low_rate ? (i < end ? (e ? 0u : 65534u) : 0u) : e;
-    }
-    __syncthreads();
-    walsh_lds(v, u);
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint32_t p = uint32_t(v[i]) * lw_fold[i];
-        uint32_t f = add_mod(p & 0xFFFFu, p >> 16);
-        if (low_rate && i == 0) f = add_mod(f, lw0);
-        v[i] = f;
-    }
-    __syncthreads();
-    walsh_lds(v, u);
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
-        rowinfo[i] = v[i] | ((state[i] & 2u) ? 0u : 0x10000u);
-}
-
 __global__ void k_mul(uint8_t *rows, uint64_t packs, const uint32_t *t) {
     const uint64_t pk = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (pk >= packs) return;
@@ -973,29 +727,6 @@ hipError_t launch_pass(int K, int flags, const PassArgs &A, hipStream_t s) {
         case 6: return launch_shape<6>(narrow, flags, A, s);
         default: return hipErrorInvalidValue;
     }
-}
-
-hipError_t launch_chain(int mode, int K0, int K1, int spl, const ChainArgs &C, hipStream_t s) {
-    switch (mode) {
-        case kChainEncodeHigh: return launch_chain_m<kChainEncodeHigh>(K0, K1, spl, C, s);
-        case kChainEncodeLow: return launch_chain_m<kChainEncodeLow>(K0, K1, spl, C, s);
-        case kChainDecode: return launch_chain_m<kChainDecode>(K0, K1, spl, C, s);
-        default: return hipErrorNotSupported;
-    }
-}
-
-hipError_t launch_eval_poly(uint32_t u, bool low_rate, uint32_t end, const uint8_t *state, const uint16_t *lw_fold_u,
-                            uint16_t log_walsh0, uint32_t *rowinfo, hipStream_t s) {
-    const size_t lds = size_t(2) << u;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_eval_poly),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 2 << 16);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
-    k_eval_poly<<<1, 1024, lds, s>>>(u, low_rate ? 1u : 0u, end, state, lw_fold_u, log_walsh0, rowinfo);
-    return hipGetLastError();
 }
 
 hipError_t launch_mul(uint8_t *rows, uint64_t blocks, const uint32_t *t, hipStream_t s) {

@@ -7,8 +7,8 @@
 // whole encode -- IFFT (engine_naive.rs:75-105), chunk XOR-fold / replicate
 // (rate_high.rs:56-74, rate_low.rs:59-78), FFT (engine_naive.rs:43-73) -- or
 // decode (rate_high.rs:172-254) runs inside one workgroup: there is no
-// cross-workgroup hand-off, which is what bounds the multi-pass / chain
-// kernels at small shard matrices (DESIGN.md "Column kernel").
+// cross-workgroup hand-off, which is what bounds the multi-pass kernels at
+// small shard matrices (DESIGN.md "Column kernel").
 //
 // Rows live in registers: a lane holds R = 2^LR rows; row-index bits are
 // spread over register bits, the 6 lane bits and the wave bits.  A butterfly

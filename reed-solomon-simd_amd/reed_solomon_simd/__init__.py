@@ -122,14 +122,7 @@ def profile_collect(ctx=None, max_records: int = 1 << 16):
     return [(nm[i].decode(), float(ms[i]), int(by[i])) for i in range(max(n, 0))]
 
 
-_sig("rs_chain_enable", _int, _vp, _int)
 _sig("rs_check_device", _int, _vp)
-
-
-def chain_enable(enable: bool = True, ctx=None) -> None:
-    """Allow (default) or forbid the one-launch chain kernel for small transforms."""
-    ctx = ctx or default_context()
-    _lib.rs_chain_enable(ctx.handle, 1 if enable else 0)
 
 
 _sig("rs_mono_enable", _int, _vp, _int)

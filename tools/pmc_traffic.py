@@ -22,7 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    """'void rs::(anonymous namespace)::k_chain<5, 5, 4, 0>(rs::ChainArgs)' -> 'k_chain<5, 5, 4, 0>'"""
+    """'void rs::(anonymous namespace)::k_mono<10, 1, 0, true>(rs::MonoArgs)' -> 'k_mono<10, 1, 0, true>'"""
     m = re.search(r"(k_[a-z_]+(?:<[^()]*>)?)\(", name)
     return m.group(1) if m else name[:80]
 
