@@ -61,6 +61,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-decode", action="store_true")
+    p.add_argument("--no-host", action="store_true", help="skip the host-memory end-to-end measurement")
     p.add_argument("--profile-steps", type=int, default=50)
     return p.parse_args()
 
@@ -173,6 +174,36 @@ def main():
             w, _ = timed(dec, args.steps, args.warmup)
             decode[f"{pct}pct"] = round(step_bytes * args.steps * world / w / 2**30, 3)
 
+    # ---- host-memory end to end (pinned buffers, PCIe both ways) -------------
+    host_e2e = None
+    if not args.no_host:
+        h_o = d_orig.cpu().pin_memory()
+        h_r = torch.empty((M, S), dtype=torch.uint8).pin_memory()
+        best = None
+        for sl in (1, 2, 4, 8):
+            rs.encode_host(N, M, S, h_o, h_r, slices=sl, ctx=ctx)
+            it = max(5, args.steps // 10)
+            t0 = time.perf_counter()
+            for _ in range(it):
+                rs.encode_host(N, M, S, h_o, h_r, slices=sl, ctx=ctx)
+            dt = (time.perf_counter() - t0) / it
+            if best is None or dt < best[1]:
+                best = (sl, dt)
+        L = -(-min(N, M) // 100)
+        op = rs.present_mask([1] * (N - L) + [0] * L)
+        rp = rs.present_mask([1] * L + [0] * (M - L))
+        h_x = torch.empty((N, S), dtype=torch.uint8).pin_memory()
+        h_rc = d_rec.cpu().pin_memory()
+        rs.decode_host(N, M, S, h_o, op, h_rc, rp, h_x, slices=best[0], ctx=ctx)
+        it = max(5, args.steps // 10)
+        t0 = time.perf_counter()
+        for _ in range(it):
+            rs.decode_host(N, M, S, h_o, op, h_rc, rp, h_x, slices=best[0], ctx=ctx)
+        ddt = (time.perf_counter() - t0) / it
+        host_e2e = {"encode_GiBps": round(world * step_bytes / best[1] / 2**30, 3),
+                    "decode_1pct_GiBps": round(world * step_bytes / ddt / 2**30, 3), "slices": best[0],
+                    "note": "pinned host buffers, hipMemcpy2DAsync in + kernels + out, column slices over 3 streams"}
+
     # ---- CPU baseline (rank 0, N = 1 only) ----------------------------------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -189,6 +220,7 @@ def main():
                        "parallelism": f"replicas x{world} (independent stripes)"},
             "gpu_event_ms_per_step": round(gpu_t / args.steps * 1e3, 5),
             "decode_GiBps": decode,
+            "host_e2e": host_e2e,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

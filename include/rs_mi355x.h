@@ -175,6 +175,26 @@ rs_status rs_decode_device_strided(rs_context *ctx, rs_rate rate, uint64_t origi
                                    const uint8_t *recovery_present, void *d_restored, uint64_t restored_stride,
                                    void *stream, rs_error *err);
 
+/* ---- host-memory pipeline (shards arrive from a socket or file) ----
+ * h_original (original_count x shard_bytes) and h_recovery (recovery_count x
+ * shard_bytes) are row-major HOST matrices; pinned memory (rs_host_alloc,
+ * hipHostMalloc) gives full PCIe rate, pageable memory works but is staged by
+ * the runtime.  The byte axis is cut into `slices` column slices of whole
+ * 64-byte blocks (0 = 1); slice k is copied in, coded and copied out on its
+ * own stream, overlapping neighbouring slices.  Blocking: returns when the
+ * outputs are in host memory.  shard_bytes must be a multiple of 64.
+ * Decode copies in only received rows and writes only the missing originals
+ * of h_restored (original_count x shard_bytes). */
+void *rs_host_alloc(uint64_t bytes);
+void rs_host_free(void *p);
+rs_status rs_encode_host(rs_context *ctx, rs_rate rate, uint64_t original_count, uint64_t recovery_count,
+                         uint64_t shard_bytes, const void *h_original, void *h_recovery, uint32_t slices,
+                         rs_error *err);
+rs_status rs_decode_host(rs_context *ctx, rs_rate rate, uint64_t original_count, uint64_t recovery_count,
+                         uint64_t shard_bytes, const void *h_original, const uint8_t *original_present,
+                         const void *h_recovery, const uint8_t *recovery_present, void *h_restored,
+                         uint32_t slices, rs_error *err);
+
 /* ---- Engine trait over a device shard matrix (src/engine.rs:234-291) ----
  * d_rows: shard_count rows of shard_len_64 64-byte blocks (ShardsRefMut,
  * src/engine/shards.rs:100-189).  Infallible in the reference (debug_assert on

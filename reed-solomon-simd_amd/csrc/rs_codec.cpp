@@ -126,6 +126,18 @@ struct rs_context {
     std::mutex mu;  // guards ws (device-resident API scratch)
     Workspace ws;
     // kernel timing (rs_profile_enable)
+    // host-memory pipeline (rs_encode_host / rs_decode_host), built on first use
+    struct Pipe {
+        static constexpr int kStreams = 3;
+        hipStream_t st[kStreams] = {};
+        Workspace ws[kStreams];
+        DevBuf orig, rec, out;
+        ~Pipe() {
+            for (hipStream_t s : st)
+                if (s) (void)hipStreamDestroy(s);
+        }
+    };
+    Pipe *pipe = nullptr;
     bool prof = false;
     struct Rec {
         hipEvent_t a, b;
@@ -683,6 +695,7 @@ rs_status rs_context_create(int device, rs_context **out) {
 
 void rs_context_destroy(rs_context *ctx) {
     if (!ctx) return;
+    delete ctx->pipe;
     if (ctx->d_tw) (void)hipFree(ctx->d_tw);
     if (ctx->d_lut) (void)hipFree(ctx->d_lut);
     if (ctx->d_lwfold) (void)hipFree(ctx->d_lwfold);
@@ -748,6 +761,148 @@ rs_status rs_encode_device_strided(rs_context *ctx, rs_rate rate, uint64_t N, ui
 rs_status rs_encode_device(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, const void *d_orig,
                            void *d_rec, void *stream, rs_error *err) {
     return rs_encode_device_strided(ctx, rate, N, M, S, d_orig, 0, d_rec, 0, stream, err);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// host-memory pipeline: the shard matrices live in host memory (pinned for
+// full PCIe rate).  The byte axis is cut into column slices of whole 64-byte
+// blocks (every op is column-wise, src/engine/utils.rs:35-43); slice k is
+// copied in, coded and copied out on stream k % kStreams, so the copies of
+// one slice overlap the kernels of its neighbours.
+
+namespace {
+
+rs_context::Pipe &pipe_of(rs_context *ctx) {
+    if (!ctx->pipe) {
+        auto *p = new rs_context::Pipe;
+        for (hipStream_t &s : p->st) {
+            hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+            if (e != hipSuccess) {
+                delete p;
+                check(e);
+            }
+        }
+        ctx->pipe = p;
+    }
+    return *ctx->pipe;
+}
+
+uint64_t slice_width(uint64_t S, uint32_t slices) {
+    const uint64_t blocks = S / 64;
+    const uint64_t k = std::max<uint64_t>(1, std::min<uint64_t>(slices ? slices : 1, blocks));
+    return (blocks + k - 1) / k * 64;
+}
+
+// hipMemcpy2DAsync of the rows [r0, r1) where flag[r] == want, in runs
+void copy_rows(uint8_t *dst, const uint8_t *src, uint64_t pitch, uint64_t width, const uint8_t *flag, uint8_t want,
+               uint64_t rows, hipMemcpyKind kind, hipStream_t s) {
+    uint64_t r = 0;
+    while (r < rows) {
+        if (flag && (flag[r] != 0) != (want != 0)) {
+            ++r;
+            continue;
+        }
+        uint64_t e = r + 1;
+        while (e < rows && (!flag || (flag[e] != 0) == (want != 0))) ++e;
+        check(hipMemcpy2DAsync(dst + r * pitch, pitch, src + r * pitch, pitch, width, e - r, kind, s));
+        r = e;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+void *rs_host_alloc(uint64_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void rs_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
+rs_status rs_encode_host(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, const void *h_orig,
+                         void *h_rec, uint32_t slices, rs_error *err) {
+    if (!ctx || !h_orig || !h_rec) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    const int high = resolve(rate, N, M, S, err);
+    if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
+    if (S % 64) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    return guarded(err, [&]() -> rs_status {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        ProfScope prof(ctx);
+        check(hipSetDevice(ctx->device));
+        auto &P = pipe_of(ctx);
+        auto *d_o = static_cast<uint8_t *>(P.orig.get(N * S));
+        auto *d_r = static_cast<uint8_t *>(P.rec.get(M * S));
+        const auto *h_o = static_cast<const uint8_t *>(h_orig);
+        auto *h_r = static_cast<uint8_t *>(h_rec);
+        const uint64_t w = slice_width(S, slices);
+        int k = 0;
+        for (uint64_t a = 0; a < S; a += w, ++k) {
+            const uint64_t b = std::min(S, a + w);
+            hipStream_t s = P.st[k % rs_context::Pipe::kStreams];
+            Workspace &ws = P.ws[k % rs_context::Pipe::kStreams];
+            check(hipMemcpy2DAsync(d_o + a, S, h_o + a, S, b - a, N, hipMemcpyHostToDevice, s));
+            Geom g{b - a, uint32_t((b - a) / 8)};
+            g.orig_stride = g.rec_stride = S;
+            if (high) encode_high(ctx, ws, g, N, M, d_o + a, d_r + a, s);
+            else encode_low(ctx, ws, g, N, M, d_o + a, d_r + a, s);
+            check(hipMemcpy2DAsync(h_r + a, S, d_r + a, S, b - a, M, hipMemcpyDeviceToHost, s));
+        }
+        for (hipStream_t s : P.st) check(hipStreamSynchronize(s));
+        return set_err(err, RS_OK);
+    });
+}
+
+rs_status rs_decode_host(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, const void *h_orig,
+                         const uint8_t *orig_present, const void *h_rec, const uint8_t *rec_present,
+                         void *h_restored, uint32_t slices, rs_error *err) {
+    if (!ctx || !h_orig || !h_rec || !h_restored || !orig_present || !rec_present)
+        return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    const int high = resolve(rate, N, M, S, err);
+    if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
+    if (S % 64) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    uint64_t have_o = 0, have_r = 0;
+    for (uint64_t i = 0; i < N; ++i) have_o += orig_present[i] != 0;
+    for (uint64_t i = 0; i < M; ++i) have_r += rec_present[i] != 0;
+    if (have_o + have_r < N) {
+        set_err(err, RS_ERR_NOT_ENOUGH_SHARDS);
+        if (err) err->original_count = N, err->original_received_count = have_o, err->recovery_received_count = have_r;
+        return RS_ERR_NOT_ENOUGH_SHARDS;
+    }
+    if (have_o == N) return set_err(err, RS_OK);
+    return guarded(err, [&]() -> rs_status {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        ProfScope prof(ctx);
+        check(hipSetDevice(ctx->device));
+        auto &P = pipe_of(ctx);
+        auto *d_o = static_cast<uint8_t *>(P.orig.get(N * S));
+        auto *d_r = static_cast<uint8_t *>(P.rec.get(M * S));
+        auto *d_x = static_cast<uint8_t *>(P.out.get(N * S));
+        const auto *h_o = static_cast<const uint8_t *>(h_orig);
+        const auto *h_r = static_cast<const uint8_t *>(h_rec);
+        auto *h_x = static_cast<uint8_t *>(h_restored);
+        const uint64_t w = slice_width(S, slices);
+        int k = 0;
+        for (uint64_t a = 0; a < S; a += w, ++k) {
+            const uint64_t b = std::min(S, a + w);
+            hipStream_t s = P.st[k % rs_context::Pipe::kStreams];
+            Workspace &ws = P.ws[k % rs_context::Pipe::kStreams];
+            // only received rows travel in, only restored rows travel out
+            copy_rows(d_o + a, h_o + a, S, b - a, orig_present, 1, N, hipMemcpyHostToDevice, s);
+            copy_rows(d_r + a, h_r + a, S, b - a, rec_present, 1, M, hipMemcpyHostToDevice, s);
+            Geom g{b - a, uint32_t((b - a) / 8)};
+            g.orig_stride = g.rec_stride = g.out_stride = S;
+            decode_dev(ctx, ws, high, g, N, M, d_o + a, orig_present, d_r + a, rec_present, d_x + a, s);
+            copy_rows(h_x + a, d_x + a, S, b - a, orig_present, 0, N, hipMemcpyDeviceToHost, s);
+        }
+        for (hipStream_t s : P.st) check(hipStreamSynchronize(s));
+        return set_err(err, RS_OK);
+    });
 }
 
 rs_status rs_decode_device_strided(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S,

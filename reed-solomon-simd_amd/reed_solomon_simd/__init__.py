@@ -653,6 +653,49 @@ def decode_device(original_count: int, recovery_count: int, shard_bytes: int, d_
                                          _stream(stream), ctypes.byref(err)), err)
 
 
+_sig("rs_host_alloc", ctypes.c_void_p, _u64)
+_sig("rs_host_free", None, ctypes.c_void_p)
+_sig("rs_encode_host", _int, _vp, _int, _u64, _u64, _u64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+     ctypes.POINTER(_RsError))
+_sig("rs_decode_host", _int, _vp, _int, _u64, _u64, _u64, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p,
+     ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(_RsError))
+
+
+def _host_ptr(x) -> int:
+    """Address of a contiguous host buffer: numpy array, torch CPU tensor (pinned for full rate) or int."""
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        if x.is_cuda or not x.is_contiguous():
+            raise ValueError("host buffers must be contiguous CPU tensors")
+        return x.data_ptr()
+    if not x.flags["C_CONTIGUOUS"]:
+        raise ValueError("host buffers must be C-contiguous")
+    return x.ctypes.data
+
+
+def encode_host(original_count: int, recovery_count: int, shard_bytes: int, h_original, h_recovery,
+                slices: int = 4, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None) -> None:
+    """Encode shard matrices in HOST memory (rs_encode_host): column slices pipelined over
+    H2D copy / kernels / D2H copy on several streams.  Blocks until h_recovery is filled."""
+    ctx = ctx or default_context()
+    err = _RsError()
+    _raise(_lib.rs_encode_host(ctx.handle, rate_, original_count, recovery_count, shard_bytes,
+                               _host_ptr(h_original), _host_ptr(h_recovery), slices, ctypes.byref(err)), err)
+
+
+def decode_host(original_count: int, recovery_count: int, shard_bytes: int, h_original, original_present,
+                h_recovery, recovery_present, h_restored, slices: int = 4, rate_: int = RATE_DEFAULT,
+                ctx: Optional[Context] = None) -> None:
+    """Decode from HOST memory (rs_decode_host); only missing originals of h_restored are written."""
+    ctx = ctx or default_context()
+    err = _RsError()
+    _raise(_lib.rs_decode_host(ctx.handle, rate_, original_count, recovery_count, shard_bytes,
+                               _host_ptr(h_original), present_mask(original_present), _host_ptr(h_recovery),
+                               present_mask(recovery_present), _host_ptr(h_restored), slices,
+                               ctypes.byref(err)), err)
+
+
 def _sharded_encode(original_count, recovery_count, shard_bytes, d_original, d_recovery, encode_slice, group=None):
     """Column-partitioned encode over the ranks of `group`.
 

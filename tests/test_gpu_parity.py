@@ -562,3 +562,35 @@ def test_column_kernel_and_pass_paths_match_oracle(torch, rs, rate, N, M, S, mon
             assert np.all(dg[~miss] == 0x33), "present rows of the output must not be written"
     finally:
         rs.mono_enable(1)
+
+
+# ---------------------------------------------------------------------------
+# host-memory pipeline (column slices over several streams, pinned or pageable buffers)
+
+@pytest.mark.parametrize("rate,N,M,S,slices,pinned", [
+    ("default", 1024, 1024, 1024, 4, True), ("default", 1024, 1024, 1024, 1, False), ("high", 3000, 700, 640, 3, True),
+    ("low", 100, 1000, 192, 8, False), ("default", 5000, 300, 4096, 5, True)])
+def test_host_pipeline_matches_oracle(torch, rs, rate, N, M, S, slices, pinned):
+    orig = O.generate_original(N, S, 21)
+    want = O.encode(rate, orig, M)
+    if pinned:
+        h_o = torch.from_numpy(orig).pin_memory()
+        h_r = torch.full((M, S), 0xEE, dtype=torch.uint8).pin_memory()
+    else:
+        h_o, h_r = orig.copy(), np.full((M, S), 0xEE, np.uint8)
+    rs.encode_host(N, M, S, h_o, h_r, slices=slices, rate_=RATE[rate])
+    got = h_r.numpy() if pinned else h_r
+    assert np.array_equal(got, want)
+    rng = np.random.default_rng(N + M + S)
+    L = max(1, min(N, M) // 3)
+    op = np.ones(N, np.uint8)
+    op[rng.choice(N, L, replace=False)] = 0
+    rp = np.zeros(M, np.uint8)
+    rp[rng.choice(M, L, replace=False)] = 1
+    h_out = np.full((N, S), 0x33, np.uint8)
+    rs.decode_host(N, M, S, np.where(op[:, None] == 1, orig, 0xA5).astype(np.uint8), op,
+                   np.where(rp[:, None] == 1, want, 0x5A).astype(np.uint8), rp, h_out, slices=slices,
+                   rate_=RATE[rate])
+    miss = op == 0
+    assert np.array_equal(h_out[miss], orig[miss])
+    assert np.all(h_out[~miss] == 0x33), "present rows of the output must not be written"

@@ -19,7 +19,7 @@ fi
 timeout -k 10 300 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 cat "$OUT/bench.json"
 
-BENCH="bench.py --no-cpu --steps 200 --warmup 20"
+BENCH="bench.py --no-cpu --no-host --steps 200 --warmup 20"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/kt" -o run -- python3 $BENCH \
   > "$OUT/kt.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d "$OUT/pmc_fetch" -o run -- python3 $BENCH \
