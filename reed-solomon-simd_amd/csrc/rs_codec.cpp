@@ -205,14 +205,19 @@ rs::PassArgs base_args(rs_context *ctx, const Geom &g, uint32_t n) {
 // low to high: level k covers transform-row bits [lo_k, lo_k + K_k).  The
 // IFFT runs levels 0..m-1 ascending, the FFT m-1..0 descending; the top
 // level's IFFT + FFT are fused into one pass (DESIGN.md "Pass structure").
-constexpr uint32_t kMaxK = 6;
+constexpr uint32_t kMaxK = 8;  // pass kernels exist for K <= 8
+// Default 6: 7- and 8-bit passes (fewer HBM round trips) measured slower
+// overall -- 32768:32768 x 1 KiB encode 116 vs 85 us, 8192:8192 x 64 KiB
+// decode 3.24 vs 2.79 ms (profiles/r01g/sweep_k8.jsonl vs sweep_k6.jsonl).
+uint32_t g_max_k = 6;           // RS_MI355X_MAX_K (4..8)
 struct Levels {
     uint32_t m = 0;
     uint32_t lo[4] = {0, 0, 0, 0}, K[4] = {0, 0, 0, 0};
 };
 Levels levels(uint32_t L) {
     Levels v;
-    v.m = L == 0 ? 1 : (L + kMaxK - 1) / kMaxK;
+    const uint32_t mk = g_max_k;
+    v.m = L == 0 ? 1 : (L + mk - 1) / mk;
     // the fused top level does two transforms: give it the smallest share
     uint32_t rest = L;
     for (uint32_t k = 0; k < v.m; ++k) {
@@ -314,7 +319,7 @@ void launch_mono(int mode, uint32_t L, const rs::MonoArgs &M, hipStream_t s, uin
     check(rs::launch_mono(mode, int(L), M, s));
     if (t_prof_ctx) {
         static thread_local char buf[64];
-        snprintf(buf, sizeof buf, "k_mono<%u, %d, %d, %s>", L, rs::mono_rows_log2_per_lane(int(L)), mode,
+        snprintf(buf, sizeof buf, "k_mono<%u, %d, %d, %s>", L, rs::mono_rows_log2_per_lane(int(L), M.chunks), mode,
                  rs::mono_staged(int(L), M.chunks) ? "true" : "false");
         prof_end(s, ev, buf, bytes);
     }
@@ -459,6 +464,29 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
     uint64_t received = 0, missing = 0;
     for (uint32_t r = 0; r < nd; ++r) received += st[r] == 2;
     for (uint64_t i = 0; i < N; ++i) missing += !orig_present[i];
+    const rs::RowMap rec_map{rec, g.rec(), high ? 0u : chunk, high ? uint32_t(M) : end};
+    const rs::RowMap orig_map{orig, g.orig(), high ? chunk : 0u, high ? end : uint32_t(N)};
+    const rs::RowMap out_map{restored, g.out(), orig_map.row_begin, orig_map.row_end};
+    const bool mono = use_mono(ctx, u, g, 1);
+    if (mono && rs::mono_staged(int(u), 1) && nd <= rs::kMonoFusedRows) {
+        // one launch: every column workgroup evaluates eval_poly itself
+        rs::MonoArgs Mo = mono_args(ctx, u, g);
+        Mo.src[0] = rec_map;
+        Mo.src[1] = orig_map;
+        Mo.nsrc = 2;
+        Mo.dst = out_map;
+        Mo.fused_eval = 1;
+        Mo.low_rate = high ? 0 : 1;
+        Mo.end = end;
+        Mo.lw0 = ctx->lw0;
+        Mo.lw_fold = ctx->d_lwfold + (nd - 1);
+        for (uint32_t r = 0; r < nd; ++r) {
+            Mo.erased[r >> 5] |= uint32_t(st[r] == 1) << (r & 31);
+            Mo.received[r >> 5] |= uint32_t(st[r] == 2) << (r & 31);
+        }
+        launch_mono(rs::kMonoDecode, u, Mo, s, (received + missing) * uint64_t(g.packs) * 8);
+        return;
+    }
     uint32_t *d_rowinfo = static_cast<uint32_t *>(ws.rowinfo.get(size_t(nd) * 4));
     rs::EvalArgs E;
     E.u = u;
@@ -485,10 +513,7 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
 
     rs::PassArgs A = base_args(ctx, g, nd);
     A.rowinfo = d_rowinfo;
-    const rs::RowMap rec_map{rec, g.rec(), high ? 0u : chunk, high ? uint32_t(M) : end};
-    const rs::RowMap orig_map{orig, g.orig(), high ? chunk : 0u, high ? end : uint32_t(N)};
-    const rs::RowMap out_map{restored, g.out(), orig_map.row_begin, orig_map.row_end};
-    if (use_mono(ctx, u, g, 1)) {
+    if (mono) {
         rs::MonoArgs Mo = mono_args(ctx, u, g);
         Mo.src[0] = rec_map;
         Mo.src[1] = orig_map;
@@ -680,6 +705,10 @@ rs_status rs_context_create(int device, rs_context **out) {
         ctx->lw0 = T.log_walsh[0];
         const char *nm = getenv("RS_MI355X_NO_MONO");
         ctx->mono = !(nm && nm[0] == '1');
+        if (const char *mk = getenv("RS_MI355X_MAX_K")) {
+            const unsigned long k = strtoul(mk, nullptr, 10);
+            if (k >= 4 && k <= kMaxK) g_max_k = uint32_t(k);
+        }
         const char *ma = getenv("RS_MI355X_MONO_ALL");
         ctx->mono_all = ma && ma[0] == '1';
         if (const char *mp = getenv("RS_MI355X_MONO_MAX_PACKS")) ctx->mono_max_packs = uint32_t(strtoul(mp, nullptr, 10));

@@ -76,6 +76,7 @@ hipError_t launch_pass(int K, int flags, const PassArgs &args, hipStream_t strea
 // layer b = 0..L-1 and group g < n / 2^(b+1), the perm table of skew index
 // g * 2^(b+1) + 2^b + t * n - 1 at table slot n - n / 2^b + g.
 enum MonoMode { kMonoEncodeHigh = 0, kMonoEncodeLow = 1, kMonoDecode = 2 };
+constexpr uint32_t kMonoFusedRows = 2048;  // largest work size of the fused-eval_poly decode
 struct MonoArgs {
     uint32_t packs = 0;          // packs per row (shard_bytes / 8, rounded up)
     uint32_t packs_per_xcd = 0;  // ceil(packs / 8): workgroup b runs pack (b % 8) * packs_per_xcd + b / 8
@@ -89,12 +90,19 @@ struct MonoArgs {
     uint32_t fft_img = 0, fft_img_step = 0;
     const uint32_t *rowinfo = nullptr;  // decode: bits 0-15 log factor, bit 16 erased
     const uint32_t *lut = nullptr;      // perm tables by log factor (Engine::mul semantics)
+    // decode with eval_poly fused into the staged kernel (every workgroup
+    // evaluates it; no rowinfo): erased / received bits of the 2^L work rows,
+    // as in EvalArgs
+    uint32_t fused_eval = 0, low_rate = 0, end = 0, lw0 = 0;
+    const uint16_t *lw_fold = nullptr;
+    uint32_t erased[kMonoFusedRows / 32] = {}, received[kMonoFusedRows / 32] = {};
 };
 // hipErrorNotSupported: no column kernel for this L (7 <= L <= 12 are built).
 hipError_t launch_mono(int mode, int L, const MonoArgs &A, hipStream_t stream);
-// Variant launch_mono picks: LDS-staged twiddles (single chunk, 2 rows per lane).
+// Variant launch_mono picks: LDS-staged twiddles (single chunk, 2 rows per
+// lane, L <= 11); fused_eval requires it.
 bool mono_staged(int L, uint32_t chunks);
-int mono_rows_log2_per_lane(int L);
+int mono_rows_log2_per_lane(int L, uint32_t chunks);
 
 // eval_poly for a decode (src/engine/utils.rs:20-31) reduced to 2^u points
 // (DESIGN.md "eval_poly"): erasure vector -> per-row log factors.

@@ -5,8 +5,8 @@
 // (DESIGN.md "eval_poly").  All arithmetic is mod 65535; 0 and 65535 are the
 // same residue and every consumer treats them alike.
 //
-// One workgroup; the Walsh-Hadamard layers run 3 at a time in registers
-// (8 values per thread per round), rounds meet in LDS.
+// One workgroup of up to 1024 threads; one Walsh-Hadamard layer per barrier
+// over LDS; every global read (bitmaps, folded log_walsh) is issued up front.
 #include <hip/hip_runtime.h>
 
 #include "rs_device.hpp"
@@ -34,44 +34,50 @@ __device__ __forceinline__ uint32_t sub_mod(uint32_t a, uint32_t b) {
     return (d + (d >> 16)) & 0xFFFFu;
 }
 
-// Q layers of the transform on bits [a, a + Q) for every group of 2^Q values.
-template <int Q>
-__device__ __forceinline__ void walsh_round(uint16_t *v, uint32_t u, uint32_t a) {
-    const uint32_t groups = 1u << (u - Q);
-    for (uint32_t g = threadIdx.x; g < groups; g += blockDim.x) {
-        const uint32_t base = (g & ((1u << a) - 1u)) | ((g >> a) << (a + Q));
-        uint32_t x[1 << Q];
-#pragma unroll
-        for (int j = 0; j < (1 << Q); ++j) x[j] = v[base + (uint32_t(j) << a)];
-#pragma unroll
-        for (int l = 0; l < Q; ++l)
-#pragma unroll
-            for (int j = 0; j < (1 << Q); ++j)
-                if (!(j & (1 << l))) {
-                    const uint32_t p = x[j], q = x[j | (1 << l)];
-                    x[j] = add_mod(p, q);
-                    x[j | (1 << l)] = sub_mod(p, q);
-                }
-#pragma unroll
-        for (int j = 0; j < (1 << Q); ++j) v[base + (uint32_t(j) << a)] = uint16_t(x[j]);
-    }
-    __syncthreads();
-}
-
+// One Walsh-Hadamard layer per barrier on bit h of 2^u values in LDS: every
+// thread takes the butterflies t, t + T, ... (pairs (i, i + 2^h)).
 __device__ void walsh(uint16_t *v, uint32_t u) {
-    uint32_t a = 0;
-    for (; a + 3 <= u; a += 3) walsh_round<3>(v, u, a);
-    if (u - a == 2) walsh_round<2>(v, u, a);
-    else if (u - a == 1) walsh_round<1>(v, u, a);
+    const uint32_t half = 1u << (u - 1);
+    for (uint32_t h = 0; h < u; ++h) {
+        for (uint32_t k = threadIdx.x; k < half; k += blockDim.x) {
+            const uint32_t i = ((k >> h) << (h + 1)) | (k & ((1u << h) - 1u));
+            const uint32_t p = v[i], q = v[i + (1u << h)];
+            v[i] = uint16_t(add_mod(p, q));
+            v[i + (1u << h)] = uint16_t(sub_mod(p, q));
+        }
+        __syncthreads();
+    }
 }
 
+// LDS: v[2^u] u16 values, then the erased / received bitmaps (2^u bits each).
 __global__ void __launch_bounds__(1024) k_eval_poly(const EvalArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint16_t v[];
     const uint32_t n = 1u << A.u;
     const bool inl = n <= kEvalInlineRows;
+    uint32_t *bits = reinterpret_cast<uint32_t *>(v + (n < 2 ? 2 : n));  // [0, nw): erased, [nw, 2nw): received
+    const uint32_t nw = (n + 31) / 32;
     RS_ESTAMP(0);
+    // every global read is issued up front: one memory latency, not one per phase
+    uint32_t lw[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t i = threadIdx.x + uint32_t(k) * blockDim.x;
+        lw[k] = i < n ? A.lw_fold[i] : 0u;
+    }
+    if (inl) {
+        for (uint32_t w = threadIdx.x; w < 2 * nw; w += blockDim.x)
+            bits[w] = w < nw ? A.erased[w] : A.received[w - nw];
+    } else {
+        for (uint32_t w = threadIdx.x; w < 2 * nw; w += blockDim.x) {
+            const uint32_t base = (w % nw) * 32, sh = w < nw ? 0 : 1;
+            uint32_t x = 0;
+            for (uint32_t j = 0; j < 32 && base + j < n; ++j) x |= ((A.state[base + j] >> sh) & 1u) << j;
+            bits[w] = x;
+        }
+    }
+    __syncthreads();
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint32_t e = inl ? (A.erased[i >> 5] >> (i & 31)) & 1u : A.state[i] & 1u;
+        const uint32_t e = (bits[i >> 5] >> (i & 31)) & 1u;
         // high rate: v = e;  low rate: v = e - 1 on [0, end), 0 beyond  (mod 65535)
         v[i] = uint16_t(A.low_rate ? (i < A.end ? (e ? 0u : 65534u) : 0u) : e);
     }
@@ -79,8 +85,8 @@ __global__ void __launch_bounds__(1024) k_eval_poly(const EvalArgs A) {
     RS_ESTAMP(1);
     walsh(v, A.u);
     RS_ESTAMP(2);
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint32_t p = uint32_t(v[i]) * A.lw_fold[i];
+    for (uint32_t i = threadIdx.x, k = 0; i < n; i += blockDim.x, ++k) {
+        const uint32_t p = uint32_t(v[i]) * (k < 8 ? lw[k & 7] : A.lw_fold[i]);
         uint32_t f = add_mod(p & 0xFFFFu, p >> 16);
         if (A.low_rate && i == 0) f = add_mod(f, A.lw0);
         v[i] = uint16_t(f);
@@ -90,7 +96,7 @@ __global__ void __launch_bounds__(1024) k_eval_poly(const EvalArgs A) {
     walsh(v, A.u);
     RS_ESTAMP(4);
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint32_t rcv = inl ? (A.received[i >> 5] >> (i & 31)) & 1u : (A.state[i] >> 1) & 1u;
+        const uint32_t rcv = (bits[nw + (i >> 5)] >> (i & 31)) & 1u;
         A.rowinfo[i] = v[i] | (rcv ? 0u : 0x10000u);
     }
     RS_ESTAMP(5);
@@ -99,16 +105,17 @@ __global__ void __launch_bounds__(1024) k_eval_poly(const EvalArgs A) {
 }  // namespace
 
 hipError_t launch_eval_poly(const EvalArgs &A, hipStream_t s) {
-    const size_t lds = size_t(2) << A.u;
+    const uint32_t n = 1u << A.u;
+    const size_t lds = size_t(2) * (n < 2 ? 2 : n) + size_t(8) * ((n + 31) / 32);
     static bool attr_set = false;  // benign race: idempotent attribute call
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_eval_poly),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 2 << 16);
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    const uint32_t threads = A.u >= 13 ? 1024 : (A.u >= 4 ? 1u << (A.u - 3) : 1);
-    k_eval_poly<<<1, threads < 64 ? 64 : threads, lds, s>>>(A);
+    const uint32_t threads = n / 2 >= 1024 ? 1024 : (n / 2 < 64 ? 64 : n / 2);
+    k_eval_poly<<<1, threads, lds, s>>>(A);
     return hipGetLastError();
 }
 

@@ -674,19 +674,21 @@ hipError_t launch_k(int flags, const PassArgs &A, hipStream_t s) {
     }
 }
 
-// Two shapes per K: "wide" (64-pack slices, 8 rows per lane) for matrices
-// that fill the chip, "narrow" (16..32-pack slices, 2 rows per lane, in-wave
-// phase changes by lane transposes) to spread small matrices over more
-// workgroups and waves.
+// Two shapes per K: "wide" (64-pack slices, 32 at K = 8, 8 rows per lane)
+// for matrices that fill the chip, "narrow" (16..32-pack slices, 2 rows per
+// lane -- 4 at K = 8 -- in-wave phase changes by lane transposes) to spread
+// small matrices over more workgroups and waves.  At most 1024 threads and
+// 160 KiB of LDS: K = 8 wide is 1024 threads, 64 KiB plane + 4 x 20 KiB tables.
 template <int K>
 hipError_t launch_shape(bool narrow, int flags, const PassArgs &A, hipStream_t s) {
     constexpr int LRW = K < 3 ? K : 3;
+    constexpr int SPLW = K >= 8 ? 5 : 6;
     if constexpr (K >= 2) {
-        constexpr int LRN = 1;
+        constexpr int LRN = K >= 8 ? 2 : 1;
         constexpr int SPLN = 6 - (K - LRN) > 4 ? 6 - (K - LRN) : 4;
         if (narrow) return launch_k<K, LRN, SPLN>(flags, A, s);
     }
-    return launch_k<K, LRW, 6>(flags, A, s);
+    return launch_k<K, LRW, SPLW>(flags, A, s);
 }
 
 
@@ -725,6 +727,8 @@ hipError_t launch_pass(int K, int flags, const PassArgs &A, hipStream_t s) {
         case 4: return launch_shape<4>(narrow, flags, A, s);
         case 5: return launch_shape<5>(narrow, flags, A, s);
         case 6: return launch_shape<6>(narrow, flags, A, s);
+        case 7: return launch_shape<7>(narrow, flags, A, s);
+        case 8: return launch_shape<8>(narrow, flags, A, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -297,14 +297,18 @@ struct Stage {
     static constexpr uint32_t n = 1u << L, W = 1u << IW;
     // layers of the last (FFT) in-wave phase
     static constexpr int NB3 = WB > 0 ? WB : L;
-    static constexpr uint32_t kPriv = W - 1;                       // tables per wave region
-    static constexpr uint32_t kP3 = W - (W >> NB3);                  // tables of phase 3
+    // B0 = 1: layer 0 of phases 1 and 3 (one table per butterfly) is read from
+    // the global image instead, so the private regions fit LDS at L = 11
+    static constexpr int B0 = L >= 11 ? 1 : 0;
+    static constexpr uint32_t kPriv = (W >> B0) - 1;                 // tables per wave region
+    static constexpr uint32_t kP3 = (W >> B0) - (W >> NB3);          // tables of phase 3
     static constexpr uint32_t kShI = WB > 0 ? (n >> IW) - 1 : 0;     // shared: IFFT layers IW..L-1
     static constexpr uint32_t kShF = WB > 0 ? (n >> WB) - 1 : 0;     // shared: FFT layers WB..L-1
     static constexpr uint32_t kShared = kShI + kShF;
     static constexpr uint32_t kWaves = 1u << (L - LR - 6);
     static constexpr uint32_t plane_words = 2 * n;
     static constexpr uint32_t words = plane_words + (kShared + kWaves * kPriv) * 20;
+    static constexpr uint32_t words_dec = words + n;  // + per-row decode info (fused eval_poly)
 };
 
 // Table source: tables staged in LDS (STAGED column kernel).  Phase 1 (IFFT
@@ -315,13 +319,16 @@ struct Stage {
 template <int L, int LR>
 struct LdsTabs {
     using G = Stage<L, LR>;
-    const uint32_t *priv, *shared;
+    const uint32_t *priv, *shared, *img_i, *img_f;
     template <int, int, typename S, int I, int PH>
     __device__ __forceinline__ void get(int x, uint32_t row, uint32_t (&t)[20]) const {
         uint32_t slot;
         const uint32_t *base;
-        if constexpr (PH == 1 || PH == 3) {
-            slot = G::W - (G::W >> x) + ((row & (G::W - 1)) >> (x + 1));
+        if constexpr ((PH == 1 || PH == 3) && G::B0 == 1 && S::v.ops[I].bit == 0) {
+            load_tab(PH == 1 ? img_i : img_f, L, 0, row, t);
+            return;
+        } else if constexpr (PH == 1 || PH == 3) {
+            slot = (G::W >> G::B0) - (G::W >> x) + ((row & (G::W - 1)) >> (x + 1));
             base = priv;
         } else if constexpr (PH == 2) {
             slot = (G::n >> G::IW) - (G::n >> x) + (row >> (x + 1));
@@ -456,11 +463,15 @@ __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR> &c, uint32_t *p
         constexpr int I = decltype(ic)::value;
         constexpr Op op = S::v.ops[I];
         if constexpr (op.kind == kOpXpose) {
+#ifndef RS_MONO_SKIP_XPOSE  // tools/mono_probe.hip ablation
             apply_xpose<L, LR, S, I>(c, lane);
+#endif
         } else if constexpr (op.kind == kOpRemap) {
             pre_remap();
             RS_MSTAMP(FFT ? 8 : 3);
+#ifndef RS_MONO_SKIP_REMAP  // tools/mono_probe.hip ablation
             apply_remap<L, LR, S, I>(c, plane, lane, wave);
+#endif
             RS_MSTAMP(FFT ? 9 : 4);
             prime(std::integral_constant<int, NL1>{}, std::integral_constant<int, NL>{});
         } else {
@@ -490,85 +501,124 @@ __device__ __forceinline__ const uint8_t *row_ptr(const MonoArgs &A, uint32_t r)
     return p;
 }
 
-// Load transform rows `chunk * n + row` (placement: start of the IFFT).
-// SCALE (decode): erased rows load as zero, received rows are multiplied by
-// exp(log factor) (rate_high.rs:213-231).
-template <int L, int LR, bool SCALE>
-__device__ __forceinline__ void load_col(const MonoArgs &A, uint32_t chunk, uint32_t pk_off, Col<L, LR> &c,
-                                         uint32_t lane, uint32_t wave) {
+// Row I/O pairs lanes: lanes 2k and 2k+1 read / write the low and the high
+// word of the SAME row (one 64-byte block, one cache line) in one
+// instruction, so a wave instruction touches 32 lines instead of 64 -- the
+// column kernel's row I/O is bound by lines per instruction.  A 2x2 transpose
+// (register pair x lane bit 0) converts between that order and the
+// placement's (low, high) of a lane's own rows.
+template <typename S, int I, int LR>
+__device__ __forceinline__ uint32_t paired_row(uint32_t lane, uint32_t wave, int j) {
+    return lane_rows<S, I>((lane & ~1u) | uint32_t(j & 1), wave) | reg_rows<S, I, LR>(j >> 1);
+}
+
+// Load transform rows `chunk * n + row` (placement: start of the IFFT) as
+// paired words; finish_col completes them.  Missing rows inside the caller's
+// matrices are read and discarded by the decode's scaling.
+template <int L, int LR>
+__device__ __forceinline__ void issue_col(const MonoArgs &A, uint32_t chunk, uint32_t pk_off,
+                                          uint32_t (&w)[2 << LR], uint32_t lane, uint32_t wave) {
     using S = SeqOf<L, LR, false>;
-    const uint32_t a = lane_rows<S, 0>(lane, wave) + chunk * (1u << L);
-    uint32_t f[1 << LR];
-    static_for<0, (1 << LR)>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        const uint32_t r = a | reg_rows<S, 0, LR>(i);
+    const uint32_t base = chunk * (1u << L);
+    const uint32_t half = (lane & 1u) * 32u;
+    static_for<0, (2 << LR)>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const uint32_t r = paired_row<S, 0, LR>(lane, wave, j) + base;
         const uint8_t *p = row_ptr(A, r);
-        if constexpr (SCALE) {
-            f[i] = A.rowinfo[r];
-            if (f[i] & 0x10000u) p = nullptr;
-        }
-        uint32_t l = 0, h = 0;
+        uint32_t v = 0;
 #ifdef RS_MONO_SKIP_IO
         p = nullptr;
-        l = r * 0x9E3779B9u, h = r;
+        v = r * 0x9E3779B9u + half;
 #endif
-        if (p) {
-            l = *reinterpret_cast<const uint32_t *>(p + pk_off);
-            h = *reinterpret_cast<const uint32_t *>(p + pk_off + 32);
-        }
-        c.lo[i] = l;
-        c.hi[i] = h;
+        if (p) v = *reinterpret_cast<const uint32_t *>(p + pk_off + half);
+        w[j] = v;
+    });
+}
+
+// SCALE (decode): erased rows become zero, received rows are multiplied by
+// exp(log factor) (rate_high.rs:213-231); rowinfo is indexed by work row.
+template <int L, int LR, bool SCALE>
+__device__ __forceinline__ void finish_col(const MonoArgs &A, const uint32_t *rowinfo, uint32_t (&w)[2 << LR],
+                                           Col<L, LR> &c, uint32_t lane, uint32_t wave) {
+    using S = SeqOf<L, LR, false>;
+    constexpr int R = 1 << LR;
+    static_for<0, R>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        xpose<0>(w[2 * i], w[2 * i + 1], lane);
+        c.lo[i] = w[2 * i];
+        c.hi[i] = w[2 * i + 1];
     });
     if constexpr (SCALE) {
-        static_for<0, (1 << LR)>([&](auto ic) {
+        const uint32_t a = lane_rows<S, 0>(lane, wave);
+        static_for<0, R>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
+            const uint32_t f = rowinfo[a | reg_rows<S, 0, LR>(i)];
             uint32_t t[20];
-            const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + (f[i] & 0xFFFFu) * 5u;
+            const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + (f & 0xFFFFu) * 5u;
 #pragma unroll
-            for (int w = 0; w < 5; ++w) {
-                const uint4 v = q[w];
-                t[4 * w] = v.x, t[4 * w + 1] = v.y, t[4 * w + 2] = v.z, t[4 * w + 3] = v.w;
+            for (int v = 0; v < 5; ++v) {
+                const uint4 x = q[v];
+                t[4 * v] = x.x, t[4 * v + 1] = x.y, t[4 * v + 2] = x.z, t[4 * v + 3] = x.w;
             }
             gf_mul4(c.lo[i], c.hi[i], t);
+            if (f & 0x10000u) c.lo[i] = c.hi[i] = 0;
         });
     }
 }
 
+template <int L, int LR, bool SCALE>
+__device__ __forceinline__ void load_col(const MonoArgs &A, uint32_t chunk, uint32_t pk_off, Col<L, LR> &c,
+                                         uint32_t lane, uint32_t wave) {
+    uint32_t w[2 << LR];
+    issue_col<L, LR>(A, chunk, pk_off, w, lane, wave);
+    finish_col<L, LR, SCALE>(A, A.rowinfo, w, c, lane, wave);
+}
+
 // Store transform rows `chunk * n + row` that fall in A.dst (placement: end
-// of the FFT).  REVEAL (decode): only erased rows, multiplied by
-// exp(65535 - log factor) (rate_high.rs:241-245).
+// of the FFT), paired like the loads.  REVEAL (decode): only erased rows,
+// multiplied by exp(65535 - log factor) (rate_high.rs:241-245).
 template <int L, int LR, bool REVEAL>
-__device__ __forceinline__ void store_col(const MonoArgs &A, uint32_t chunk, uint32_t pk_off, Col<L, LR> &c,
-                                          uint32_t lane, uint32_t wave) {
+__device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *rowinfo, uint32_t chunk,
+                                          uint32_t pk_off, Col<L, LR> &c, uint32_t lane, uint32_t wave) {
     using S = SeqOf<L, LR, true>;
-    const uint32_t a = lane_rows<S, S::v.count>(lane, wave) + chunk * (1u << L);
-    static_for<0, (1 << LR)>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        const uint32_t r = a | reg_rows<S, S::v.count, LR>(i);
-        if (r >= A.dst.row_begin && r < A.dst.row_end) {
-            uint8_t *p = const_cast<uint8_t *>(A.dst.base) + uint64_t(r - A.dst.row_begin) * A.dst.stride + pk_off;
-            uint32_t l = c.lo[i], h = c.hi[i];
-            bool keep = true;
-            if constexpr (REVEAL) {
-                const uint32_t f = A.rowinfo[r];
-                keep = f & 0x10000u;
-                if (keep) {
-                    uint32_t t[20];
-                    const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + (65535u - (f & 0xFFFFu)) * 5u;
+    constexpr int I = S::v.count;
+    constexpr int R = 1 << LR;
+    const uint32_t base = chunk * (1u << L);
+    if constexpr (REVEAL) {
+        const uint32_t a = lane_rows<S, I>(lane, wave) + base;
+        static_for<0, R>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            const uint32_t f = rowinfo[a | reg_rows<S, I, LR>(i)];
+            uint32_t t[20];
+            const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + (65535u - (f & 0xFFFFu)) * 5u;
 #pragma unroll
-                    for (int w = 0; w < 5; ++w) {
-                        const uint4 v = q[w];
-                        t[4 * w] = v.x, t[4 * w + 1] = v.y, t[4 * w + 2] = v.z, t[4 * w + 3] = v.w;
-                    }
-                    gf_mul4(l, h, t);
-                }
+            for (int v = 0; v < 5; ++v) {
+                const uint4 x = q[v];
+                t[4 * v] = x.x, t[4 * v + 1] = x.y, t[4 * v + 2] = x.z, t[4 * v + 3] = x.w;
             }
+            gf_mul4(c.lo[i], c.hi[i], t);
+        });
+    }
+    uint32_t w[2 * R];
+    static_for<0, R>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        w[2 * i] = c.lo[i];
+        w[2 * i + 1] = c.hi[i];
+        xpose<0>(w[2 * i], w[2 * i + 1], lane);
+    });
+    const uint32_t half = (lane & 1u) * 32u;
+    static_for<0, 2 * R>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const uint32_t r = paired_row<S, I, LR>(lane, wave, j) + base;
+        if (r >= A.dst.row_begin && r < A.dst.row_end) {
+            bool keep = true;
+            if constexpr (REVEAL) keep = rowinfo[r] & 0x10000u;
 #ifdef RS_MONO_SKIP_IO
-            keep = (l ^ h) == 0x12345678u;
+            keep = w[j] == 0x12345678u;
 #endif
             if (keep) {
-                *reinterpret_cast<uint32_t *>(p) = l;
-                *reinterpret_cast<uint32_t *>(p + 32) = h;
+                uint8_t *p = const_cast<uint8_t *>(A.dst.base) + uint64_t(r - A.dst.row_begin) * A.dst.stride;
+                *reinterpret_cast<uint32_t *>(p + pk_off + half) = w[j];
             }
         }
     });
@@ -606,6 +656,83 @@ __device__ __forceinline__ void formal_derivative(Col<L, LR> &c, uint32_t *plane
 }
 
 // ---------------------------------------------------------------------------
+// eval_poly fused into the staged decode (rs_eval.hip has the standalone
+// kernel; same reduction to 2^L points, src/engine/utils.rs:20-31).  Thread t
+// holds work rows 2t and 2t+1 (2 rows per lane), so the Walsh-Hadamard layer
+// on row bit 0 runs in registers, bits 1..6 across lanes, and the wave bits
+// through LDS ping-pong buffers (one barrier per bit).  Mod 65535 throughout.
+__device__ __forceinline__ uint32_t ev_add(uint32_t a, uint32_t b) {
+    const uint32_t s = a + b;
+    return (s + (s >> 16)) & 0xFFFFu;
+}
+__device__ __forceinline__ uint32_t ev_sub(uint32_t a, uint32_t b) {
+    const uint32_t d = a - b;
+    return (d + (d >> 16)) & 0xFFFFu;
+}
+
+template <int L>
+__device__ __forceinline__ void col_walsh(uint32_t (&x)[2], uint32_t *buf) {
+    const uint32_t t = threadIdx.x;
+    {
+        const uint32_t p = x[0], q = x[1];
+        x[0] = ev_add(p, q);
+        x[1] = ev_sub(p, q);
+    }
+    static_for<1, (L < 7 ? L : 7)>([&](auto jc) {
+        constexpr uint32_t m = 1u << (decltype(jc)::value - 1);  // lane bit of row bit j
+        const bool up = t & m;
+        static_for<0, 2>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const uint32_t y = uint32_t(__shfl_xor(int(x[k]), int(m)));
+            x[k] = up ? ev_sub(y, x[k]) : ev_add(x[k], y);
+        });
+    });
+    static_for<7, (L > 7 ? L : 7)>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        constexpr uint32_t h = 1u << (j - 1);  // thread bit of row bit j
+        uint32_t *b = buf + ((j & 1) << L);
+        b[2 * t] = x[0];
+        b[2 * t + 1] = x[1];
+        __syncthreads();
+        const bool up = t & h;
+        const uint32_t pt = t ^ h;
+        const uint32_t y0 = b[2 * pt], y1 = b[2 * pt + 1];
+        x[0] = up ? ev_sub(y0, x[0]) : ev_add(x[0], y0);
+        x[1] = up ? ev_sub(y1, x[1]) : ev_add(x[1], y1);
+    });
+}
+
+// rinfo[r] = log factor | (received ? 0 : 0x10000) for the 2^L work rows.
+// ebits / rbits: this thread's erased / received bits (bits 0, 1 = rows 2t,
+// 2t+1); lw: lw_fold of those rows.  Ends with a barrier.
+template <int L>
+__device__ __forceinline__ void col_eval_poly(const MonoArgs &A, uint32_t ebits, uint32_t rbits,
+                                              const uint32_t (&lw)[2], uint32_t *buf, uint32_t *rinfo) {
+    const uint32_t i0 = 2 * threadIdx.x;
+    uint32_t x[2];
+    static_for<0, 2>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const uint32_t e = (ebits >> k) & 1u, i = i0 + k;
+        // high rate: v = e;  low rate: v = e - 1 on [0, end), 0 beyond  (rate_low.rs:196)
+        x[k] = A.low_rate ? (i < A.end ? (e ? 0u : 65534u) : 0u) : e;
+    });
+    col_walsh<L>(x, buf);
+    static_for<0, 2>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const uint32_t p = x[k] * lw[k];
+        uint32_t f = ev_add(p & 0xFFFFu, p >> 16);
+        if (A.low_rate && i0 + k == 0) f = ev_add(f, A.lw0);
+        x[k] = f;
+    });
+    col_walsh<L>(x, buf);
+    static_for<0, 2>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        rinfo[i0 + k] = x[k] | (((rbits >> k) & 1u) ? 0u : 0x10000u);
+    });
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
 // LDS staging of the twiddle tables (STAGED kernel): 16-byte pieces q of the
 // wave-private region (phase 1 from the IFFT image, phase 3 from the FFT
 // image) and of the shared region.
@@ -613,9 +740,9 @@ template <int L, int LR>
 __device__ __forceinline__ uint4 priv_piece(const uint32_t *img, uint32_t wave, uint32_t q) {
     using G = Stage<L, LR>;
     const uint32_t t = q / 5, piece = q - t * 5;
-    const uint32_t y = G::W - t;                              // in [1, W]
+    const uint32_t y = (G::W >> G::B0) - t;                   // in [1, W >> B0]
     const int b = G::IW - int(32 - __builtin_clz(y - 1));    // IW - ceil(log2 y)
-    const uint32_t local = t - (G::W - (G::W >> b));
+    const uint32_t local = t - ((G::W >> G::B0) - (G::W >> b));
     const uint32_t slot = G::n - (G::n >> b) + wave * (G::W >> (b + 1)) + local;
     return reinterpret_cast<const uint4 *>(img)[slot * 5u + piece];
 }
@@ -651,35 +778,59 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
     const uint32_t *img_f = A.img + uint64_t(A.fft_img) * A.img_words;
     C c;
     if constexpr (STAGED) {
-        // one chunk in, one chunk out; every table read comes from LDS
+        // one chunk in, one chunk out; every table read comes from LDS (layer
+        // 0 of phases 1 / 3 from the image when Stage::B0)
         constexpr bool DEC = MODE == kMonoDecode;
-        RS_MSTAMP(0);
-        load_col<L, LR, DEC>(A, 0, pk_off, c, lane, wave);
         uint32_t *shared = lds + G::plane_words;
         uint32_t *priv = shared + G::kShared * 20 + wave * G::kPriv * 20;
+        uint32_t *rinfo = lds + G::words;  // decode with fused eval_poly
         constexpr int KP1 = (5 * G::kPriv + 63) / 64, KP3 = (5 * G::kP3 + 63) / 64;
         constexpr int KSH = G::kShared ? (5 * G::kShared + T - 1) / T : 1;
-        {
-            uint4 v1[KP1], vs[KSH];
-            static_for<0, KP1>([&](auto kc) {
-                const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < 5 * G::kPriv) v1[kc] = priv_piece<L, LR>(img_i, wave, q);
-            });
-            static_for<0, KSH>([&](auto kc) {
-                const uint32_t q = threadIdx.x + T * decltype(kc)::value;
-                if (q < 5 * G::kShared) vs[kc] = shared_piece<L, LR>(img_i, img_f, q);
-            });
-            static_for<0, KP1>([&](auto kc) {
-                const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < 5 * G::kPriv) reinterpret_cast<uint4 *>(priv)[q] = v1[kc];
-            });
-            static_for<0, KSH>([&](auto kc) {
-                const uint32_t q = threadIdx.x + T * decltype(kc)::value;
-                if (q < 5 * G::kShared) reinterpret_cast<uint4 *>(shared)[q] = vs[kc];
-            });
+        RS_MSTAMP(0);
+        // every global read is requested before any of them is waited for
+        uint32_t ebits = 0, rbits = 0, lw[2] = {0, 0};
+        if constexpr (DEC) {
+            if (A.fused_eval) {
+                const uint32_t i0 = 2 * threadIdx.x;
+                ebits = A.erased[i0 >> 5] >> (i0 & 31);
+                rbits = A.received[i0 >> 5] >> (i0 & 31);
+                lw[0] = A.lw_fold[i0];
+                lw[1] = A.lw_fold[i0 + 1];
+            }
         }
+        uint32_t w[2 << LR];
+        issue_col<L, LR>(A, 0, pk_off, w, lane, wave);
+        uint4 v1[KP1], vs[KSH];
+#ifndef RS_MONO_SKIP_STAGE  // tools/mono_probe.hip ablation
+        static_for<0, KP1>([&](auto kc) {
+            const uint32_t q = lane + 64u * decltype(kc)::value;
+            if (q < 5 * G::kPriv) v1[kc] = priv_piece<L, LR>(img_i, wave, q);
+        });
+        static_for<0, KSH>([&](auto kc) {
+            const uint32_t q = threadIdx.x + T * decltype(kc)::value;
+            if (q < 5 * G::kShared) vs[kc] = shared_piece<L, LR>(img_i, img_f, q);
+        });
+#endif
+        const uint32_t *ri = A.rowinfo;
+        if constexpr (DEC) {
+            if (A.fused_eval) {
+                col_eval_poly<L>(A, ebits, rbits, lw, plane, rinfo);
+                ri = rinfo;
+            }
+        }
+#ifndef RS_MONO_SKIP_STAGE
+        static_for<0, KP1>([&](auto kc) {
+            const uint32_t q = lane + 64u * decltype(kc)::value;
+            if (q < 5 * G::kPriv) reinterpret_cast<uint4 *>(priv)[q] = v1[kc];
+        });
+        static_for<0, KSH>([&](auto kc) {
+            const uint32_t q = threadIdx.x + T * decltype(kc)::value;
+            if (q < 5 * G::kShared) reinterpret_cast<uint4 *>(shared)[q] = vs[kc];
+        });
+#endif
+        finish_col<L, LR, DEC>(A, ri, w, c, lane, wave);
         RS_MSTAMP(1);
-        const LdsTabs<L, LR> ts{priv, shared};
+        const LdsTabs<L, LR> ts{priv, shared, img_i, img_f};
         // phase-3 tables: requested when phase 1 ends, written over this wave's
         // phase-1 tables when phase 2 ends
         uint4 v3[KP3];
@@ -708,7 +859,7 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             run_seq<L, LR, true, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, NoHook{});
         }
         RS_MSTAMP(10);
-        store_col<L, LR, DEC>(A, 0, pk_off, c, lane, wave);
+        store_col<L, LR, DEC>(A, ri, 0, pk_off, c, lane, wave);
         RS_MSTAMP(11);
     } else if constexpr (MODE == kMonoEncodeHigh) {
         // rate_high.rs:44-87: recovery = FFT_0(XOR_c IFFT_{c n + n}(chunk c))
@@ -725,7 +876,7 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             });
         }
         run_seq<L, LR, true, kMonoPrefetch>(GlobalTabs{img_f}, c, plane, lane, wave, NoHook{});
-        store_col<L, LR, false>(A, 0, pk_off, c, lane, wave);
+        store_col<L, LR, false>(A, A.rowinfo, 0, pk_off, c, lane, wave);
     } else if constexpr (MODE == kMonoEncodeLow) {
         // rate_low.rs:44-87: recovery chunk c = FFT_{c n + n}(IFFT_0(original))
         load_col<L, LR, false>(A, 0, pk_off, c, lane, wave);
@@ -734,7 +885,7 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             C t = c;
             run_seq<L, LR, true, kMonoPrefetch>(
                 GlobalTabs{img_f + uint64_t(ch) * A.fft_img_step * A.img_words}, t, plane, lane, wave, NoHook{});
-            store_col<L, LR, false>(A, ch, pk_off, t, lane, wave);
+            store_col<L, LR, false>(A, A.rowinfo, ch, pk_off, t, lane, wave);
         }
     } else {
         // rate_high.rs:213-245 / rate_low.rs:213-245 after eval_poly
@@ -742,20 +893,30 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
         run_seq<L, LR, false, kMonoPrefetch>(GlobalTabs{img_i}, c, plane, lane, wave, NoHook{});
         formal_derivative<L, LR>(c, plane, lane, wave);
         run_seq<L, LR, true, kMonoPrefetch>(GlobalTabs{img_f}, c, plane, lane, wave, NoHook{});
-        store_col<L, LR, true>(A, 0, pk_off, c, lane, wave);
+        store_col<L, LR, true>(A, A.rowinfo, 0, pk_off, c, lane, wave);
     }
 }
 
 #ifndef RS_MONO_LR10
 #define RS_MONO_LR10 1
 #endif
-// log2 rows per lane: 2^(L - LR) threads, at most 512
-constexpr int mono_lr(int L) { return L <= 10 ? (RS_MONO_LR10 < L - 6 ? RS_MONO_LR10 : L - 6) : L - 9; }
+#ifndef RS_MONO_NO_STAGE
+#define RS_MONO_STAGED_MAX_L 11
+#else
+#define RS_MONO_STAGED_MAX_L 0
+#endif
+// log2 rows per lane (2^(L - LR) threads, at most 1024): the staged variant
+// keeps 2 rows per lane (L <= 11); the unstaged one at most 512 threads
+constexpr bool staged_l(int L) { return L <= RS_MONO_STAGED_MAX_L && (L >= 11 || RS_MONO_LR10 == 1); }
+constexpr int mono_lr(int L, bool staged) {
+    return staged ? 1 : L <= 10 ? (RS_MONO_LR10 < L - 6 ? RS_MONO_LR10 : L - 6) : L - 9;
+}
 
 template <int L, int MODE, bool STAGED>
 hipError_t launch_ls(const MonoArgs &A, hipStream_t s) {
-    constexpr int LR = mono_lr(L);
-    const size_t lds = STAGED ? size_t(Stage<L, LR>::words) * 4 : size_t(8) << L;
+    constexpr int LR = mono_lr(L, STAGED);
+    const size_t lds = STAGED ? size_t(MODE == kMonoDecode ? Stage<L, LR>::words_dec : Stage<L, LR>::words) * 4
+                              : size_t(8) << L;
     static bool attr_set = false;  // benign race: idempotent attribute call
     if (!attr_set && lds > 65536) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mono<L, LR, MODE, STAGED>),
@@ -768,16 +929,13 @@ hipError_t launch_ls(const MonoArgs &A, hipStream_t s) {
     return hipGetLastError();
 }
 
-#ifndef RS_MONO_NO_STAGE
-#define RS_MONO_STAGED_MAX_L 10
-#else
-#define RS_MONO_STAGED_MAX_L 0
-#endif
-// Staged (LDS tables) variant: single-chunk transforms with 2 rows per lane.
+// Staged (LDS tables) variant: single-chunk transforms, 2 rows per lane.
 template <int L, int MODE>
 hipError_t launch_l(const MonoArgs &A, hipStream_t s) {
-    if constexpr (L <= RS_MONO_STAGED_MAX_L && mono_lr(L) == 1) {
+    if constexpr (staged_l(L)) {
         if (A.chunks == 1) return launch_ls<L, MODE, true>(A, s);  // = mono_staged()
+    } else if (A.fused_eval) {
+        return hipErrorInvalidValue;
     }
     return launch_ls<L, MODE, false>(A, s);
 }
@@ -797,8 +955,8 @@ hipError_t launch_m(int L, const MonoArgs &A, hipStream_t s) {
 
 }  // namespace
 
-bool mono_staged(int L, uint32_t chunks) { return L <= RS_MONO_STAGED_MAX_L && mono_lr(L) == 1 && chunks == 1; }
-int mono_rows_log2_per_lane(int L) { return mono_lr(L); }
+bool mono_staged(int L, uint32_t chunks) { return L >= 7 && staged_l(L) && chunks == 1; }
+int mono_rows_log2_per_lane(int L, uint32_t chunks) { return mono_lr(L, mono_staged(L, chunks)); }
 
 hipError_t launch_mono(int mode, int L, const MonoArgs &A, hipStream_t s) {
     if (A.packs == 0) return hipSuccess;

@@ -38,19 +38,30 @@ void run(const char *name, F &&f) {
            std::chrono::duration<double, std::micro>(t1 - t0).count() / iters);
 }
 
+__global__ void klds(int x) {
+    extern __shared__ uint32_t l[];
+    if (x) l[threadIdx.x] = x;
+}
+
 int main() {
     uint32_t *p;
     hipMalloc(&p, 4);
     Big B{};
     hipStream_t s;
     hipStreamCreate(&s);
+    hipFuncSetAttribute(reinterpret_cast<const void *>(&klds), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     run("k0 <<<256,256>>>", [&] { k0<<<256, 256>>>(); });
-    run("k1 ptr", [&] { k1<<<256, 256>>>(p); });
-    run("k8 8 args", [&] { k8<<<256, 256>>>(p, 1, 2, 3, 4, p, 5, p); });
     run("kbig 240B struct", [&] { kbig<<<256, 256>>>(B); });
-    run("kbig 240B struct, stream", [&] { kbig<<<256, 256, 0, s>>>(B); });
-    run("kbig + dyn LDS 20KB", [&] { kbig<<<256, 256, 20480, s>>>(B); });
     run("k0 x3", [&] { k0<<<256, 256>>>(); k0<<<256, 256>>>(); k0<<<256, 256>>>(); });
-    run("kbig x3 stream", [&] { kbig<<<256, 256, 0, s>>>(B); kbig<<<256, 256, 0, s>>>(B); kbig<<<256, 256, 0, s>>>(B); });
+    const int grids[] = {8, 128, 256};
+    const int blocks[] = {64, 256, 512, 1024};
+    const int ldss[] = {0, 16384, 65536, 100352, 163840};
+    for (int g : grids)
+        for (int b : blocks)
+            for (int l : ldss) {
+                char name[64];
+                snprintf(name, sizeof name, "klds grid %d block %d lds %d", g, b, l);
+                run(name, [&] { klds<<<g, b, l, s>>>(0); });
+            }
     return 0;
 }

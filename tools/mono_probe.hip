@@ -23,6 +23,11 @@
         }                                                                            \
     } while (0)
 
+__global__ void k_empty_lds(int x) {
+    extern __shared__ uint32_t lds_[];
+    if (x) lds_[threadIdx.x] = x;
+}
+
 int main(int argc, char **argv) {
     const uint32_t n = argc > 1 ? atoi(argv[1]) : 1024, S = argc > 2 ? atoi(argv[2]) : 1024;
     uint32_t L = 0;
@@ -69,6 +74,19 @@ int main(int argc, char **argv) {
     float ms;
     CK(hipEventElapsedTime(&ms, a, b));
     printf("mono encode n=%u S=%u: %.2f us/launch (back-to-back)\n", n, S, ms * 1000 / iters);
+    {  // floor: an empty kernel with the same grid, block and LDS
+        const size_t lds = size_t(rs::Stage<10, 1>::words) * 4;
+        CK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_empty_lds), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               int(lds)));
+        const uint32_t grid = 8 * A.packs_per_xcd;
+        for (int i = 0; i < 20; ++i) k_empty_lds<<<grid, 512, lds, 0>>>(0);
+        CK(hipEventRecord(a, 0));
+        for (int i = 0; i < iters; ++i) k_empty_lds<<<grid, 512, lds, 0>>>(0);
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        CK(hipEventElapsedTime(&ms, a, b));
+        printf("empty kernel, same grid/block/LDS: %.2f us/launch (back-to-back)\n", ms * 1000 / iters);
+    }
 #ifdef RS_MONO_STAMPS
     CK(hipDeviceSynchronize());
     go();
