@@ -149,6 +149,10 @@ def main():
     alg_step = (N + M) * S
     kernel_s_per_step = sum(v[0] for v in agg.values()) / 1e3 / args.profile_steps
     if len(agg) == 1 and kernels[dom]["launches_per_step"] == 1:
+        # one launch per step: its duration is the step's GPU time measured
+        # around the whole timed batch on the launch stream (gpu_t); events
+        # bracketing every single launch add their own gaps (kernels[...].avg_us)
+        dom_avg_s = gpu_t / args.steps
         scope, achieved = "launch", alg_step / dom_avg_s / 1e9
     else:
         scope, achieved = "step (all launches)", alg_step / kernel_s_per_step / 1e9

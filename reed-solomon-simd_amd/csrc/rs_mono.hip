@@ -670,35 +670,64 @@ __device__ __forceinline__ uint32_t ev_sub(uint32_t a, uint32_t b) {
     return (d + (d >> 16)) & 0xFFFFu;
 }
 
+// Value of lane ^ 2^J (no LDS traffic except the J = 2 swizzle).
+template <int J>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v, uint32_t lane) {
+    if constexpr (J == 4) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16u) ? r[0] : r[1];
+    } else if constexpr (J == 5) {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32u) ? r[0] : r[1];
+    } else {
+        return xor_lane<J>(v);
+    }
+}
+
 template <int L>
 __device__ __forceinline__ void col_walsh(uint32_t (&x)[2], uint32_t *buf) {
-    const uint32_t t = threadIdx.x;
+    const uint32_t t = threadIdx.x, lane = t & 63u;
     {
         const uint32_t p = x[0], q = x[1];
         x[0] = ev_add(p, q);
         x[1] = ev_sub(p, q);
     }
     static_for<1, (L < 7 ? L : 7)>([&](auto jc) {
-        constexpr uint32_t m = 1u << (decltype(jc)::value - 1);  // lane bit of row bit j
-        const bool up = t & m;
+        constexpr int J = decltype(jc)::value - 1;  // lane bit of row bit j
+        const bool up = lane & (1u << J);
         static_for<0, 2>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
-            const uint32_t y = uint32_t(__shfl_xor(int(x[k]), int(m)));
+            const uint32_t y = lane_xor<J>(x[k], lane);
             x[k] = up ? ev_sub(y, x[k]) : ev_add(x[k], y);
         });
     });
-    static_for<7, (L > 7 ? L : 7)>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        constexpr uint32_t h = 1u << (j - 1);  // thread bit of row bit j
-        uint32_t *b = buf + ((j & 1) << L);
+    // wave bits: two layers per LDS round (each thread reads its group's 3
+    // partners), ping-pong buffers so one barrier per round suffices
+    static_for<0, ((L > 7 ? L - 7 : 0) + 1) / 2>([&](auto rc) {
+        constexpr int rnd = decltype(rc)::value;
+        constexpr int j = 7 + 2 * rnd;               // row bits j (and j + 1)
+        constexpr bool two = j + 1 < L;
+        constexpr uint32_t h1 = 1u << (j - 1), h2 = two ? 1u << j : 0u;  // thread bits
+        uint32_t *b = buf + ((rnd & 1) << L);
         b[2 * t] = x[0];
         b[2 * t + 1] = x[1];
         __syncthreads();
-        const bool up = t & h;
-        const uint32_t pt = t ^ h;
-        const uint32_t y0 = b[2 * pt], y1 = b[2 * pt + 1];
-        x[0] = up ? ev_sub(y0, x[0]) : ev_add(x[0], y0);
-        x[1] = up ? ev_sub(y1, x[1]) : ev_add(x[1], y1);
+        const bool u1 = t & h1, u2 = t & h2;
+        static_for<0, 2>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            if constexpr (!two) {
+                const uint32_t y = b[2 * (t ^ h1) + k];
+                x[k] = u1 ? ev_sub(y, x[k]) : ev_add(x[k], y);
+            } else {
+                // v[b2][b1] of the group; this thread is (u2, u1)
+                const uint32_t g0 = t & ~(h1 | h2);
+                const uint32_t v00 = b[2 * g0 + k], v01 = b[2 * (g0 | h1) + k];
+                const uint32_t v10 = b[2 * (g0 | h2) + k], v11 = b[2 * (g0 | h1 | h2) + k];
+                const uint32_t lo = u1 ? ev_sub(v00, v01) : ev_add(v00, v01);  // layer on bit j
+                const uint32_t hi = u1 ? ev_sub(v10, v11) : ev_add(v10, v11);
+                x[k] = u2 ? ev_sub(lo, hi) : ev_add(lo, hi);                   // layer on bit j + 1
+            }
+        });
     });
 }
 
@@ -724,6 +753,7 @@ __device__ __forceinline__ void col_eval_poly(const MonoArgs &A, uint32_t ebits,
         if (A.low_rate && i0 + k == 0) f = ev_add(f, A.lw0);
         x[k] = f;
     });
+    if constexpr (L > 7) __syncthreads();  // the first transform's last LDS reads are done
     col_walsh<L>(x, buf);
     static_for<0, 2>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
@@ -788,15 +818,14 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
         constexpr int KSH = G::kShared ? (5 * G::kShared + T - 1) / T : 1;
         RS_MSTAMP(0);
         // every global read is requested before any of them is waited for
+        // (no branches between them: a branch would make the compiler wait)
         uint32_t ebits = 0, rbits = 0, lw[2] = {0, 0};
-        if constexpr (DEC) {
-            if (A.fused_eval) {
-                const uint32_t i0 = 2 * threadIdx.x;
-                ebits = A.erased[i0 >> 5] >> (i0 & 31);
-                rbits = A.received[i0 >> 5] >> (i0 & 31);
-                lw[0] = A.lw_fold[i0];
-                lw[1] = A.lw_fold[i0 + 1];
-            }
+        if constexpr (DEC) {  // the staged decode always evaluates eval_poly itself
+            const uint32_t i0 = 2 * threadIdx.x;
+            ebits = A.erased[i0 >> 5] >> (i0 & 31);
+            rbits = A.received[i0 >> 5] >> (i0 & 31);
+            lw[0] = A.lw_fold[i0];
+            lw[1] = A.lw_fold[i0 + 1];
         }
         uint32_t w[2 << LR];
         issue_col<L, LR>(A, 0, pk_off, w, lane, wave);
@@ -813,10 +842,8 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
 #endif
         const uint32_t *ri = A.rowinfo;
         if constexpr (DEC) {
-            if (A.fused_eval) {
-                col_eval_poly<L>(A, ebits, rbits, lw, plane, rinfo);
-                ri = rinfo;
-            }
+            col_eval_poly<L>(A, ebits, rbits, lw, plane, rinfo);
+            ri = rinfo;
         }
 #ifndef RS_MONO_SKIP_STAGE
         static_for<0, KP1>([&](auto kc) {
@@ -932,11 +959,14 @@ hipError_t launch_ls(const MonoArgs &A, hipStream_t s) {
 // Staged (LDS tables) variant: single-chunk transforms, 2 rows per lane.
 template <int L, int MODE>
 hipError_t launch_l(const MonoArgs &A, hipStream_t s) {
+    // the staged decode evaluates eval_poly itself; the unstaged one reads rowinfo
     if constexpr (staged_l(L)) {
-        if (A.chunks == 1) return launch_ls<L, MODE, true>(A, s);  // = mono_staged()
-    } else if (A.fused_eval) {
-        return hipErrorInvalidValue;
+        if (A.chunks == 1) {  // = mono_staged()
+            if (MODE == kMonoDecode && !A.fused_eval) return hipErrorInvalidValue;
+            return launch_ls<L, MODE, true>(A, s);
+        }
     }
+    if (A.fused_eval) return hipErrorInvalidValue;
     return launch_ls<L, MODE, false>(A, s);
 }
 

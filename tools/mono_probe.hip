@@ -61,8 +61,36 @@ int main(int argc, char **argv) {
     A.img_words = words;
     A.ifft_img = 1;
     A.fft_img = 0;
+    // decode mode: 2^L work rows = n/2 recovery + n/2 originals (high rate),
+    // recovery all present, originals all missing (the 100 % loss pattern)
+    const bool dec = argc > 3 && argv[3][0] == 'd';
+    int mode = rs::kMonoEncodeHigh;
+    std::vector<uint32_t> lwf(n, 1);
+    uint16_t *d_lw = nullptr;
+    uint32_t *d_lut = nullptr;
+    if (dec) {
+        mode = rs::kMonoDecode;
+        A.src[0] = rs::RowMap{orig, S, 0, n / 2};
+        A.src[1] = rs::RowMap{orig, S, n / 2, n};
+        A.nsrc = 2;
+        A.dst = rs::RowMap{rec, S, n / 2, n};
+        A.ifft_img = 0;
+        A.fused_eval = 1;
+        A.end = n;
+        std::vector<uint16_t> lw(T.lw_fold.begin() + (n - 1), T.lw_fold.begin() + (2 * n - 1));
+        CK(hipMalloc(&d_lw, n * 2));
+        CK(hipMemcpy(d_lw, lw.data(), n * 2, hipMemcpyHostToDevice));
+        A.lw_fold = d_lw;
+        CK(hipMalloc(&d_lut, T.perm_by_log.size() * 4));
+        CK(hipMemcpy(d_lut, T.perm_by_log.data(), T.perm_by_log.size() * 4, hipMemcpyHostToDevice));
+        A.lut = d_lut;
+        for (uint32_t r = 0; r < n; ++r) {
+            if (r < n / 2) A.received[r >> 5] |= 1u << (r & 31);
+            else A.erased[r >> 5] |= 1u << (r & 31);
+        }
+    }
     const int iters = 1000;
-    auto go = [&] { CK(rs::launch_mono(rs::kMonoEncodeHigh, int(L), A, 0)); };
+    auto go = [&] { CK(rs::launch_mono(mode, int(L), A, 0)); };
     for (int i = 0; i < 20; ++i) go();
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
@@ -73,9 +101,9 @@ int main(int argc, char **argv) {
     CK(hipEventSynchronize(b));
     float ms;
     CK(hipEventElapsedTime(&ms, a, b));
-    printf("mono encode n=%u S=%u: %.2f us/launch (back-to-back)\n", n, S, ms * 1000 / iters);
+    printf("mono %s n=%u S=%u: %.2f us/launch (back-to-back)\n", dec ? "decode" : "encode", n, S, ms * 1000 / iters);
     {  // floor: an empty kernel with the same grid, block and LDS
-        const size_t lds = size_t(rs::Stage<10, 1>::words) * 4;
+        const size_t lds = size_t(rs::Stage<10, 1>::words_dec) * 4;
         CK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_empty_lds), hipFuncAttributeMaxDynamicSharedMemorySize,
                                int(lds)));
         const uint32_t grid = 8 * A.packs_per_xcd;
