@@ -102,10 +102,77 @@ __global__ void __launch_bounds__(1024) k_eval_poly(const EvalArgs A) {
     RS_ESTAMP(5);
 }
 
+// Large transforms (2^u > kEvalSingleRows) spread over many workgroups: the
+// two FWHT_u split into their low bits [0, K1) and high bits [K1, u), four
+// launches, one workgroup per set of 2^K values that differ only in those
+// bits (Walsh-Hadamard layers on different bits commute).  The values live in
+// `rowinfo` (u32) between launches.
+//   STEP 0: values from the erasure state, low bits
+//   STEP 1: high bits, then x lw_fold (+ log_walsh[0] at 0 for low rate)
+//   STEP 2: low bits
+//   STEP 3: high bits, then rowinfo = value | not-received bit
+constexpr uint32_t kEvalSingleRows = 2048;
+
+__device__ __forceinline__ uint32_t state_bit(const EvalArgs &A, uint32_t i, uint32_t which) {
+    if ((1u << A.u) <= kEvalInlineRows) return ((which ? A.received : A.erased)[i >> 5] >> (i & 31)) & 1u;
+    return (A.state[i] >> which) & 1u;
+}
+
+template <int STEP>
+__global__ void __launch_bounds__(512) k_walsh_part(const EvalArgs A, uint32_t a, uint32_t K) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sv[];
+    const uint32_t m = 1u << K, set = blockIdx.x;
+    const uint32_t lo = set & ((1u << a) - 1u), hi = set >> a;
+    for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
+        const uint32_t i = lo + (j << a) + (hi << (a + K));
+        uint32_t x;
+        if constexpr (STEP == 0) {
+            const uint32_t e = state_bit(A, i, 0);
+            x = A.low_rate ? (i < A.end ? (e ? 0u : 65534u) : 0u) : e;
+        } else {
+            x = A.rowinfo[i];
+        }
+        sv[j] = x;
+    }
+    __syncthreads();
+    for (uint32_t h = 0; h < K; ++h) {
+        for (uint32_t k = threadIdx.x; k < m / 2; k += blockDim.x) {
+            const uint32_t i = ((k >> h) << (h + 1)) | (k & ((1u << h) - 1u));
+            const uint32_t p = sv[i], q = sv[i + (1u << h)];
+            sv[i] = add_mod(p, q);
+            sv[i + (1u << h)] = sub_mod(p, q);
+        }
+        __syncthreads();
+    }
+    for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
+        const uint32_t i = lo + (j << a) + (hi << (a + K));
+        uint32_t x = sv[j];
+        if constexpr (STEP == 1) {
+            const uint32_t p = x * A.lw_fold[i];
+            x = add_mod(p & 0xFFFFu, p >> 16);
+            if (A.low_rate && i == 0) x = add_mod(x, A.lw0);
+        }
+        if constexpr (STEP == 3) x |= state_bit(A, i, 1) ? 0u : 0x10000u;
+        A.rowinfo[i] = x;
+    }
+}
+
 }  // namespace
 
 hipError_t launch_eval_poly(const EvalArgs &A, hipStream_t s) {
     const uint32_t n = 1u << A.u;
+    if (n > kEvalSingleRows) {
+        const uint32_t K1 = A.u / 2, K2 = A.u - K1;
+        const auto go = [&](auto kern, uint32_t a, uint32_t K) {
+            const uint32_t m = 1u << K;
+            kern<<<n >> K, m / 2 < 64 ? 64 : (m / 2 > 512 ? 512 : m / 2), size_t(4) * m, s>>>(A, a, K);
+        };
+        go(k_walsh_part<0>, 0, K1);
+        go(k_walsh_part<1>, K1, K2);
+        go(k_walsh_part<2>, 0, K1);
+        go(k_walsh_part<3>, K1, K2);
+        return hipGetLastError();
+    }
     const size_t lds = size_t(2) * (n < 2 ? 2 : n) + size_t(8) * ((n + 31) / 32);
     static bool attr_set = false;  // benign race: idempotent attribute call
     if (!attr_set) {

@@ -299,7 +299,10 @@ struct Stage {
     static constexpr int NB3 = WB > 0 ? WB : L;
     // B0 = 1: layer 0 of phases 1 and 3 (one table per butterfly) is read from
     // the global image instead, so the private regions fit LDS at L = 11
-    static constexpr int B0 = L >= 11 ? 1 : 0;
+#ifndef RS_MONO_B0_MIN_L
+#define RS_MONO_B0_MIN_L 11
+#endif
+    static constexpr int B0 = L >= RS_MONO_B0_MIN_L ? 1 : 0;
     static constexpr uint32_t kPriv = (W >> B0) - 1;                 // tables per wave region
     static constexpr uint32_t kP3 = (W >> B0) - (W >> NB3);          // tables of phase 3
     static constexpr uint32_t kShI = WB > 0 ? (n >> IW) - 1 : 0;     // shared: IFFT layers IW..L-1
@@ -814,7 +817,8 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
         uint32_t *shared = lds + G::plane_words;
         uint32_t *priv = shared + G::kShared * 20 + wave * G::kPriv * 20;
         uint32_t *rinfo = lds + G::words;  // decode with fused eval_poly
-        constexpr int KP1 = (5 * G::kPriv + 63) / 64, KP3 = (5 * G::kP3 + 63) / 64;
+        constexpr int KP1 = (5 * G::kPriv + 63) / 64;
+        constexpr int KP3 = G::kP3 ? (5 * G::kP3 + 63) / 64 : 1;  // (guarded by q < 5 * kP3)
         constexpr int KSH = G::kShared ? (5 * G::kShared + T - 1) / T : 1;
         RS_MSTAMP(0);
         // every global read is requested before any of them is waited for
