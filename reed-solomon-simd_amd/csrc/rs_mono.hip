@@ -34,7 +34,7 @@ __device__ uint64_t g_mono_stamps[4096][16];
 #define RS_MSTAMP(i)                                                                                 \
     do {                                                                                             \
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                  \
-        if (threadIdx.x == 0 && blockIdx.x < 4096) g_mono_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime(); \
+        if (threadIdx.x == blockDim.x - 64 && blockIdx.x < 4096) g_mono_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define RS_MSTAMP(i)
@@ -234,6 +234,20 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
     else if constexpr (J == 1) return __builtin_amdgcn_update_dpp(0, int(v), 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
     else if constexpr (J == 2) return __builtin_amdgcn_ds_swizzle(int(v), 0x101F);  // lane ^ 4
     else return __builtin_amdgcn_update_dpp(0, int(v), 0x128, 0xF, 0xF, false);  // row_ror:8 = lane ^ 8
+}
+
+// Value of lane ^ 2^J (no LDS traffic except the J = 2 swizzle).
+template <int J>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v, uint32_t lane) {
+    if constexpr (J == 4) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16u) ? r[0] : r[1];
+    } else if constexpr (J == 5) {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32u) ? r[0] : r[1];
+    } else {
+        return xor_lane<J>(v);
+    }
 }
 
 // 2x2 transpose of (register pair, lane bit J): the lane with bit J clear ends
@@ -443,9 +457,12 @@ constexpr int kMonoPrefetch = RS_MONO_PF;
 // hides behind B - 1 layers of butterflies.  Requests never cross the remap:
 // the tables beyond it may not be in place yet (staged kernel).  `pre_remap`
 // runs just before the remap.
-template <int L, int LR, bool FFT, int B0, typename TS, typename PreRemap>
+// PRE0: the caller has already requested layer 0's tables into t0.  A wave
+// with `alive` false stops after the remap (its rows there are not needed).
+template <int L, int LR, bool FFT, int B0, bool PRE0 = false, typename TS, typename PreRemap>
 __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR> &c, uint32_t *plane, uint32_t lane, uint32_t wave,
-                                        const PreRemap &pre_remap) {
+                                        const PreRemap &pre_remap, const uint32_t (*t0)[20] = nullptr,
+                                        bool alive = true) {
     using S = SeqOf<L, LR, FFT>;
     constexpr int NT = (1 << LR) / 2;
     constexpr int NL = num_layers(S::v);
@@ -458,11 +475,12 @@ __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR> &c, uint32_t *p
         constexpr int k0 = decltype(k0c)::value, k1 = decltype(k1c)::value;
         static_for<k0, (k0 + B < k1 ? k0 + B : k1)>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
-            load_layer_tabs<L, LR, S, layer_at(S::v, k), FFT>(ts, lane, wave, tb[k % B]);
+            if constexpr (!(PRE0 && k == 0))
+                load_layer_tabs<L, LR, S, layer_at(S::v, k), FFT>(ts, lane, wave, tb[k % B]);
         });
     };
     prime(std::integral_constant<int, 0>{}, std::integral_constant<int, NL1>{});
-    static_for<0, S::v.count>([&](auto ic) {
+    auto step = [&](auto ic) {
         constexpr int I = decltype(ic)::value;
         constexpr Op op = S::v.ops[I];
         if constexpr (op.kind == kOpXpose) {
@@ -480,7 +498,10 @@ __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR> &c, uint32_t *p
         } else {
             constexpr int k = layer_ordinal(S::v, I);
 #ifndef RS_MONO_SKIP_LAYERS
-            apply_layer<L, LR, S, I, !FFT>(tb[k % B], c);
+            if constexpr (PRE0 && k == 0)
+                apply_layer<L, LR, S, I, !FFT>(*reinterpret_cast<const uint32_t(*)[NT][20]>(t0), c);
+            else
+                apply_layer<L, LR, S, I, !FFT>(tb[k % B], c);
 #endif
             constexpr int end = k < NL1 ? NL1 : NL;
             if constexpr (k + B < end) {
@@ -488,7 +509,23 @@ __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR> &c, uint32_t *p
                 asm volatile("" ::: "memory");  // keep the request here, ahead of its use
             }
         }
-    });
+    };
+    if constexpr (RI < S::v.count) {
+        static_for<0, RI + 1>(step);
+        if (alive) static_for<RI + 1, S::v.count>(step);
+    } else {
+        static_for<0, S::v.count>(step);
+    }
+}
+
+// Decode: does this wave hold, after the FFT's remap, any row of A.dst?
+// (there the wave's rows are one block of 2^IW consecutive rows)
+template <int L, int LR>
+__device__ __forceinline__ bool wave_stores(const MonoArgs &A, uint32_t wave) {
+    using S = SeqOf<L, LR, true>;
+    constexpr int I = S::v.count;
+    const uint32_t lo = lane_rows<S, I>(0, wave), hi = lo + (1u << (LR + 6));
+    return lo < A.dst.row_end && hi > A.dst.row_begin;
 }
 
 struct NoHook {
@@ -556,8 +593,11 @@ __device__ __forceinline__ void finish_col(const MonoArgs &A, const uint32_t *ro
         static_for<0, R>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             const uint32_t f = rowinfo[a | reg_rows<S, 0, LR>(i)];
+            // rows that are not received read one shared dummy table (log 0):
+            // the gather costs cache lines only for the rows that use it
+            const uint32_t lg = (f & 0x10000u) ? 0u : (f & 0xFFFFu);
             uint32_t t[20];
-            const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + (f & 0xFFFFu) * 5u;
+            const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + lg * 5u;
 #pragma unroll
             for (int v = 0; v < 5; ++v) {
                 const uint4 x = q[v];
@@ -591,9 +631,14 @@ __device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *row
         const uint32_t a = lane_rows<S, I>(lane, wave) + base;
         static_for<0, R>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
-            const uint32_t f = rowinfo[a | reg_rows<S, I, LR>(i)];
+            const uint32_t r = a | reg_rows<S, I, LR>(i);
+            const uint32_t f = rowinfo[r];
+            // only erased rows inside A.dst are revealed; the others read one
+            // shared dummy table (log 0), so their gathers cost no cache lines
+            const bool need = (f & 0x10000u) && r >= A.dst.row_begin && r < A.dst.row_end;
+            const uint32_t lg = need ? 65535u - (f & 0xFFFFu) : 0u;
             uint32_t t[20];
-            const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + (65535u - (f & 0xFFFFu)) * 5u;
+            const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + lg * 5u;
 #pragma unroll
             for (int v = 0; v < 5; ++v) {
                 const uint4 x = q[v];
@@ -629,32 +674,68 @@ __device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *row
 
 // Formal derivative, closed form over the whole column (src/engine/utils.rs:99-104):
 //   out[q] = x[q] ^ XOR_{b < L, q_b = 0} x[q | 2^b]   (placement: end of the IFFT)
+// Terms on register bits come from the lane's own registers, terms on lane
+// bits from the partner lane (DPP / permlane), terms on wave bits through the
+// LDS plane -- read only by the waves whose wave bit is clear.
 template <int L, int LR>
 __device__ __forceinline__ void formal_derivative(Col<L, LR> &c, uint32_t *plane, uint32_t lane, uint32_t wave) {
     using S = SeqOf<L, LR, true>;
     constexpr uint32_t n = 1u << L;
+    constexpr int R = 1 << LR;
+    constexpr Map m = S::v.maps[0];
     const uint32_t a = lane_rows<S, 0>(lane, wave);
-    __syncthreads();
-    static_for<0, (1 << LR)>([&](auto ic) {
+    constexpr bool kWaves = L > LR + 6;
+    if constexpr (kWaves) {
+        __syncthreads();  // the plane's previous readers are done
+        static_for<0, R>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            const uint32_t x = swz<L>(a | reg_rows<S, 0, LR>(i));
+            plane[x] = c.lo[i];
+            plane[n + x] = c.hi[i];
+        });
+    }
+    uint32_t l[R], h[R];
+    static_for<0, R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        const uint32_t x = swz<L>(a | reg_rows<S, 0, LR>(i));
-        plane[x] = c.lo[i];
-        plane[n + x] = c.hi[i];
-    });
-    __syncthreads();
-    static_for<0, (1 << LR)>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        const uint32_t q = a | reg_rows<S, 0, LR>(i);
-        uint32_t l = c.lo[i], h = c.hi[i];
-#pragma unroll
-        for (int b = 0; b < L; ++b)
-            if (!(q & (1u << b))) {
-                const uint32_t x = swz<L>(q | (1u << b));
-                l ^= plane[x];
-                h ^= plane[n + x];
+        l[i] = c.lo[i];
+        h[i] = c.hi[i];
+        static_for<0, LR>([&](auto sc) {  // register bits
+            constexpr int sb = decltype(sc)::value;
+            if constexpr (!((i >> sb) & 1)) {
+                l[i] ^= c.lo[i | (1 << sb)];
+                h[i] ^= c.hi[i | (1 << sb)];
             }
-        c.lo[i] = l;
-        c.hi[i] = h;
+        });
+    });
+    static_for<0, 6>([&](auto jc) {  // lane bits
+        constexpr int J = decltype(jc)::value;
+        const uint32_t keep = (lane >> J) & 1u ? 0u : ~0u;
+        static_for<0, R>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            l[i] ^= lane_xor<J>(c.lo[i], lane) & keep;
+            h[i] ^= lane_xor<J>(c.hi[i], lane) & keep;
+        });
+    });
+    if constexpr (kWaves) {
+        __syncthreads();
+        static_for<0, 4>([&](auto kc) {  // wave bits (wave-uniform branches)
+            constexpr int k = decltype(kc)::value;
+            if constexpr (m.wave[k] >= 0) {
+                if (!((wave >> k) & 1u)) {
+                    static_for<0, R>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value;
+                        const uint32_t x = swz<L>((a | reg_rows<S, 0, LR>(i)) ^ (1u << m.wave[k]));
+                        l[i] ^= plane[x];
+                        h[i] ^= plane[n + x];
+                    });
+                }
+            }
+        });
+    }
+    static_for<0, R>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        c.lo[i] = l[i];
+        c.hi[i] = h[i];
     });
 }
 
@@ -663,28 +744,30 @@ __device__ __forceinline__ void formal_derivative(Col<L, LR> &c, uint32_t *plane
 // kernel; same reduction to 2^L points, src/engine/utils.rs:20-31).  Thread t
 // holds work rows 2t and 2t+1 (2 rows per lane), so the Walsh-Hadamard layer
 // on row bit 0 runs in registers, bits 1..6 across lanes, and the wave bits
-// through LDS ping-pong buffers (one barrier per bit).  Mod 65535 throughout.
+// through LDS ping-pong buffers (two bits per barrier).  Mod 65535 throughout.
 __device__ __forceinline__ uint32_t ev_add(uint32_t a, uint32_t b) {
     const uint32_t s = a + b;
     return (s + (s >> 16)) & 0xFFFFu;
 }
-__device__ __forceinline__ uint32_t ev_sub(uint32_t a, uint32_t b) {
-    const uint32_t d = a - b;
-    return (d + (d >> 16)) & 0xFFFFu;
-}
 
-// Value of lane ^ 2^J (no LDS traffic except the J = 2 swizzle).
-template <int J>
-__device__ __forceinline__ uint32_t lane_xor(uint32_t v, uint32_t lane) {
-    if constexpr (J == 4) {
-        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-        return (lane & 16u) ? r[0] : r[1];
-    } else if constexpr (J == 5) {
-        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-        return (lane & 32u) ? r[0] : r[1];
-    } else {
-        return xor_lane<J>(v);
-    }
+// The transform reduces lazily: values stay below a bound B_k after k layers
+// (B_0 = 2^16; a layer maps a < B, b < B to a + b and a - b + M_k, M_k the
+// least multiple of 65535 >= B_k, so B_{k+1} = 2 B_k + 65535 < 2^29 for
+// k <= 11) and are folded back below 2^16 once at the end.  With the lane's
+// role as a mask m (0: lower element, ~0: upper) both outputs are
+// partner + (own ^ m) + (m & (M_k + 1)): two VALU per value and layer.
+constexpr uint64_t walsh_bound(int k) {
+    uint64_t b = 65536u;
+    for (int i = 0; i < k; ++i) b = 2 * b + 65535u;
+    return b;
+}
+template <int K>  // M_K + 1 (a template constant: folded at compile time)
+constexpr uint32_t kWalshM1 = uint32_t((walsh_bound(K) + 65534u) / 65535u * 65535u) + 1u;
+static_assert(walsh_bound(12) < (1ull << 32), "lazy Walsh-Hadamard bound");
+
+__device__ __forceinline__ uint32_t walsh_fold(uint32_t x) {
+    x = (x & 0xFFFFu) + (x >> 16);  // < 2^16 + 2^13
+    return (x & 0xFFFFu) + (x >> 16);  // < 2^16, same residue mod 65535
 }
 
 template <int L>
@@ -692,46 +775,52 @@ __device__ __forceinline__ void col_walsh(uint32_t (&x)[2], uint32_t *buf) {
     const uint32_t t = threadIdx.x, lane = t & 63u;
     {
         const uint32_t p = x[0], q = x[1];
-        x[0] = ev_add(p, q);
-        x[1] = ev_sub(p, q);
+        x[0] = p + q;
+        x[1] = p + ~q + kWalshM1<0>;
     }
     static_for<1, (L < 7 ? L : 7)>([&](auto jc) {
-        constexpr int J = decltype(jc)::value - 1;  // lane bit of row bit j
-        const bool up = lane & (1u << J);
+        constexpr int k = decltype(jc)::value;  // layer k = row bit k = lane bit k - 1
+        constexpr int J = k - 1;
+        const uint32_t m = (lane & (1u << J)) ? ~0u : 0u;
+        const uint32_t c = m & kWalshM1<k>;
         static_for<0, 2>([&](auto kc) {
-            constexpr int k = decltype(kc)::value;
-            const uint32_t y = lane_xor<J>(x[k], lane);
-            x[k] = up ? ev_sub(y, x[k]) : ev_add(x[k], y);
+            constexpr int q = decltype(kc)::value;
+            const uint32_t y = lane_xor<J>(x[q], lane);
+            x[q] = y + (x[q] ^ m) + c;
         });
     });
     // wave bits: two layers per LDS round (each thread reads its group's 3
     // partners), ping-pong buffers so one barrier per round suffices
     static_for<0, ((L > 7 ? L - 7 : 0) + 1) / 2>([&](auto rc) {
         constexpr int rnd = decltype(rc)::value;
-        constexpr int j = 7 + 2 * rnd;               // row bits j (and j + 1)
+        constexpr int j = 7 + 2 * rnd;  // row bits j (and j + 1) = layers j (and j + 1)
         constexpr bool two = j + 1 < L;
         constexpr uint32_t h1 = 1u << (j - 1), h2 = two ? 1u << j : 0u;  // thread bits
         uint32_t *b = buf + ((rnd & 1) << L);
         b[2 * t] = x[0];
         b[2 * t + 1] = x[1];
         __syncthreads();
-        const bool u1 = t & h1, u2 = t & h2;
+        const uint32_t m1 = (t & h1) ? ~0u : 0u, c1 = m1 & kWalshM1<j>;
         static_for<0, 2>([&](auto kc) {
-            constexpr int k = decltype(kc)::value;
+            constexpr int q = decltype(kc)::value;
             if constexpr (!two) {
-                const uint32_t y = b[2 * (t ^ h1) + k];
-                x[k] = u1 ? ev_sub(y, x[k]) : ev_add(x[k], y);
+                const uint32_t y = b[2 * (t ^ h1) + q];
+                x[q] = y + (x[q] ^ m1) + c1;
             } else {
                 // v[b2][b1] of the group; this thread is (u2, u1)
+                const uint32_t m2 = (t & h2) ? ~0u : 0u, c2 = m2 & kWalshM1<j + 1>;
                 const uint32_t g0 = t & ~(h1 | h2);
-                const uint32_t v00 = b[2 * g0 + k], v01 = b[2 * (g0 | h1) + k];
-                const uint32_t v10 = b[2 * (g0 | h2) + k], v11 = b[2 * (g0 | h1 | h2) + k];
-                const uint32_t lo = u1 ? ev_sub(v00, v01) : ev_add(v00, v01);  // layer on bit j
-                const uint32_t hi = u1 ? ev_sub(v10, v11) : ev_add(v10, v11);
-                x[k] = u2 ? ev_sub(lo, hi) : ev_add(lo, hi);                   // layer on bit j + 1
+                const uint32_t v00 = b[2 * g0 + q], v01 = b[2 * (g0 | h1) + q];
+                const uint32_t v10 = b[2 * (g0 | h2) + q], v11 = b[2 * (g0 | h1 | h2) + q];
+                // layer j: own-role element of each pair (v?0 lower, v?1 upper)
+                const uint32_t lo = v00 + (v01 ^ m1) + c1;
+                const uint32_t hi = v10 + (v11 ^ m1) + c1;
+                x[q] = lo + (hi ^ m2) + c2;  // layer j + 1
             }
         });
     });
+    x[0] = walsh_fold(x[0]);
+    x[1] = walsh_fold(x[1]);
 }
 
 // rinfo[r] = log factor | (received ? 0 : 0x10000) for the 2^L work rows.
@@ -833,6 +922,11 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
         }
         uint32_t w[2 << LR];
         issue_col<L, LR>(A, 0, pk_off, w, lane, wave);
+        // B0: layer 0's tables come from the image; request them with the rows
+        using SI = SeqOf<L, LR, false>;
+        uint32_t t0[R / 2][20];
+        if constexpr (G::B0)
+            load_layer_tabs<L, LR, SI, layer_at(SI::v, 0), false>(GlobalTabs{img_i}, lane, wave, t0);
         uint4 v1[KP1], vs[KSH];
 #ifndef RS_MONO_SKIP_STAGE  // tools/mono_probe.hip ablation
         static_for<0, KP1>([&](auto kc) {
@@ -846,8 +940,15 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
 #endif
         const uint32_t *ri = A.rowinfo;
         if constexpr (DEC) {
+#ifndef RS_MONO_SKIP_EVAL  // tools/mono_probe.hip ablation
             col_eval_poly<L>(A, ebits, rbits, lw, plane, rinfo);
+#else
+            rinfo[2 * threadIdx.x] = ebits & 1u ? 0x10000u : lw[0];
+            rinfo[2 * threadIdx.x + 1] = ebits & 2u ? 0x10000u : lw[1];
+            __syncthreads();
+#endif
             ri = rinfo;
+            RS_MSTAMP(2);
         }
 #ifndef RS_MONO_SKIP_STAGE
         static_for<0, KP1>([&](auto kc) {
@@ -859,6 +960,7 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             if (q < 5 * G::kShared) reinterpret_cast<uint4 *>(shared)[q] = vs[kc];
         });
 #endif
+        RS_MSTAMP(6);
         finish_col<L, LR, DEC>(A, ri, w, c, lane, wave);
         RS_MSTAMP(1);
         const LdsTabs<L, LR> ts{priv, shared, img_i, img_f};
@@ -878,10 +980,12 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             });
         };
         if constexpr (G::WB > 0) {
-            run_seq<L, LR, false, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, issue3);
+            run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 == 1>(ts, c, plane, lane, wave, issue3, t0);
             RS_MSTAMP(5);
             if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
-            run_seq<L, LR, true, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, write3);
+            const bool alive = !DEC || wave_stores<L, LR>(A, wave);
+            run_seq<L, LR, true, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, write3, nullptr, alive);
+            if (!alive) return;
         } else {
             run_seq<L, LR, false, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, NoHook{});
             issue3();

@@ -3,6 +3,7 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 
 struct Big {
     uint32_t w[60];
@@ -53,6 +54,12 @@ int main() {
     run("k0 <<<256,256>>>", [&] { k0<<<256, 256>>>(); });
     run("kbig 240B struct", [&] { kbig<<<256, 256>>>(B); });
     run("k0 x3", [&] { k0<<<256, 256>>>(); k0<<<256, 256>>>(); k0<<<256, 256>>>(); });
+    run("k1 null stream", [&] { k1<<<256, 256>>>(p); });
+    run("k1 stream s", [&] { k1<<<256, 256, 0, s>>>(p); });
+    run("k8 stream s", [&] { k8<<<256, 256, 0, s>>>(p, 1, 2, 3, 4, p, 5, p); });
+    run("kbig stream s", [&] { kbig<<<256, 256, 0, s>>>(B); });
+    run("klds 128x512 100K stream s", [&] { klds<<<128, 512, 100352, s>>>(0); });
+    if (getenv("LP_SHORT")) return 0;
     const int grids[] = {8, 128, 256};
     const int blocks[] = {64, 256, 512, 1024};
     const int ldss[] = {0, 16384, 65536, 100352, 163840};

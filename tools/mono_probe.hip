@@ -84,8 +84,11 @@ int main(int argc, char **argv) {
         CK(hipMalloc(&d_lut, T.perm_by_log.size() * 4));
         CK(hipMemcpy(d_lut, T.perm_by_log.data(), T.perm_by_log.size() * 4, hipMemcpyHostToDevice));
         A.lut = d_lut;
+        // "d1": the 1 % pattern (recovery 0..11 and originals 0..n/2-12 received)
+        const bool one = argv[3][1] == '1';
         for (uint32_t r = 0; r < n; ++r) {
-            if (r < n / 2) A.received[r >> 5] |= 1u << (r & 31);
+            const bool rcv = one ? (r < 12 || (r >= n / 2 && r < n - 11)) : r < n / 2;
+            if (rcv) A.received[r >> 5] |= 1u << (r & 31);
             else A.erased[r >> 5] |= 1u << (r & 31);
         }
     }
@@ -124,9 +127,9 @@ int main(int argc, char **argv) {
     CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(rs::g_mono_stamps), st.size() * 8));
     uint64_t t0 = ~0ull;
     for (uint32_t w = 0; w < wgs; ++w) t0 = std::min(t0, st[w * 16]);
-    const char *names[16] = {"start", "loaded", "", "ifft A done", "remap1 done", "ifft B done", "", "",
+    const char *names[16] = {"start", "loaded", "eval done", "ifft A done", "remap1 done", "ifft B done", "staged", "",
                              "fft B done", "remap2 done", "fft C done", "stored"};
-    const int order[] = {0, 1, 3, 4, 5, 8, 9, 10, 11};
+    const int order[] = {0, 2, 6, 1, 3, 4, 5, 8, 9, 10, 11};
     for (int i : order) {
         std::vector<double> v;
         for (uint32_t w = 0; w < wgs; ++w) v.push_back((st[w * 16 + i] - t0) * 0.01);
