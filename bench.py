@@ -175,8 +175,10 @@ def main():
             def dec(op=op, rp=rp):
                 rs.decode_device(N, M, S, d_orig, op, d_rec, rp, d_out, stream=stream, ctx=ctx)
 
-            w, _ = timed(dec, args.steps, args.warmup)
+            w, g = timed(dec, args.steps, args.warmup)
             decode[f"{pct}pct"] = round(step_bytes * args.steps * world / w / 2**30, 3)
+            decode[f"{pct}pct_us_per_step"] = {"wall": round(w / args.steps * 1e6, 2),
+                                               "gpu_events": round(g / args.steps * 1e6, 2)}
 
     # ---- host-memory end to end (pinned buffers, PCIe both ways) -------------
     host_e2e = None

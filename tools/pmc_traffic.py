@@ -55,7 +55,11 @@ def main(tag):
                   "launches": fetch[k][1]}
     with open(os.path.join(dst, "traffic.json"), "w") as f:
         json.dump({"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes ({tag})",
-                   "correction": "FETCH_SIZE x2 (gfx950 streaming-read half count), KiB -> bytes",
+                   "correction": "FETCH_SIZE x2 (gfx950 half count; calibrated for the column kernel's 4-byte paired-lane "
+                                 "pack reads by tools/fetch_calib.hip, profiles/r01j/fetch_calib_*.csv: a 512 MiB read "
+                                 "reports 262,155 KiB, the 16 B/lane stream 262,147 KiB), KiB -> bytes",
+                   "note": "FETCH counts L2 misses per XCD (Infinity-Cache hits included): tables read by every "
+                           "workgroup are fetched once per XCD, 8x their size",
                    "kernels": out}, f, indent=1)
     print(json.dumps(out, indent=1))
 
