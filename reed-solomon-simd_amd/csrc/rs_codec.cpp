@@ -206,11 +206,14 @@ rs::PassArgs base_args(rs_context *ctx, const Geom &g, uint32_t n) {
 // IFFT runs levels 0..m-1 ascending, the FFT m-1..0 descending; the top
 // level's IFFT + FFT are fused into one pass (DESIGN.md "Pass structure").
 constexpr uint32_t kMaxK = 8;  // pass kernels exist for K <= 8
-// Measured (profiles/r01g/sweep_k*.jsonl, profiles/r01i/): encodes gain from
-// 7-bit passes (8192:8192 x 64 KiB 747 -> 857 GiB/s), decodes lose (364 -> 314
-// GiB/s; their scale / reveal / derivative passes carry more tables), and
-// 8-bit passes lose for both (32768:32768 x 1 KiB encode 116 vs 85 us).
-uint32_t g_max_k_enc = 7, g_max_k_dec = 6;  // RS_MI355X_MAX_K overrides both (4..8)
+// Measured (profiles/r01g/sweep_k*.jsonl, profiles/r01i/, profiles/r01k/):
+// with the 512-thread wide shapes (rs_kernels.hip launch_shape), 7-bit passes
+// win for encodes (8192:8192 x 64 KiB 747 -> 857 GiB/s) and decodes (377 ->
+// 396 GiB/s); 8-bit passes only once a transform has thousands of packs
+// (32768:32768 x 64 KiB encode 820 -> 884 GiB/s; at 1 KiB shards 656 -> 505).
+uint32_t g_max_k = 0;  // RS_MI355X_MAX_K (4..8) overrides the choice below
+uint32_t max_k_enc(uint32_t packs) { return g_max_k ? g_max_k : packs >= 2048 ? 8 : 7; }
+uint32_t max_k_dec() { return g_max_k ? g_max_k : 7; }
 struct Levels {
     uint32_t m = 0;
     uint32_t lo[4] = {0, 0, 0, 0}, K[4] = {0, 0, 0, 0};
@@ -332,7 +335,7 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
                  uint8_t *rec, hipStream_t s) {
     const uint32_t n = uint32_t(next_pow2(M)), L = ilog2(n);
     const uint32_t C = uint32_t((N + n - 1) / n);
-    const Levels lv = levels(L, g_max_k_enc);
+    const Levels lv = levels(L, max_k_enc(g.packs));
     rs::PassArgs A = base_args(ctx, g, n);
     A.ifft_delta = n;
     A.ifft_delta_step = n;
@@ -387,7 +390,7 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
                 uint8_t *rec, hipStream_t s) {
     const uint32_t n = uint32_t(next_pow2(N)), L = ilog2(n);
     const uint32_t C = uint32_t((M + n - 1) / n);
-    const Levels lv = levels(L, g_max_k_enc);
+    const Levels lv = levels(L, max_k_enc(g.packs));
     rs::PassArgs A = base_args(ctx, g, n);
     A.fft_delta = n;
     A.fft_delta_step = n;
@@ -523,7 +526,7 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
         launch_mono(rs::kMonoDecode, u, Mo, s, (received + missing) * uint64_t(g.packs) * 8);
         return;
     }
-    const Levels lv = levels(u, g_max_k_dec);
+    const Levels lv = levels(u, max_k_dec());
     if (lv.m == 1) {
         A.src[0] = rec_map;
         A.src[1] = orig_map;
@@ -707,7 +710,7 @@ rs_status rs_context_create(int device, rs_context **out) {
         ctx->mono = !(nm && nm[0] == '1');
         if (const char *mk = getenv("RS_MI355X_MAX_K")) {
             const unsigned long k = strtoul(mk, nullptr, 10);
-            if (k >= 4 && k <= kMaxK) g_max_k_enc = g_max_k_dec = uint32_t(k);
+            if (k >= 4 && k <= kMaxK) g_max_k = uint32_t(k);
         }
         const char *ma = getenv("RS_MI355X_MONO_ALL");
         ctx->mono_all = ma && ma[0] == '1';
@@ -1243,7 +1246,7 @@ static rs_status engine_xform(rs_context *ctx, void *rows, uint64_t count, uint6
         const uint32_t n = uint32_t(size), L = ilog2(n);
         rs::PassArgs A = base_args(ctx, g, n);
         A.ifft_delta = A.fft_delta = uint32_t(delta);
-        const Levels lv = levels(L, g_max_k_enc);
+        const Levels lv = levels(L, max_k_enc(g.packs));
         A.work_in = A.work_out = base;
         A.work_stride = g.stride;
         // in place: IFFT runs levels low -> high, FFT high -> low

@@ -674,15 +674,17 @@ hipError_t launch_k(int flags, const PassArgs &A, hipStream_t s) {
     }
 }
 
-// Two shapes per K: "wide" (64-pack slices, 32 at K = 8, 8 rows per lane)
-// for matrices that fill the chip, "narrow" (16..32-pack slices, 2 rows per
-// lane -- 4 at K = 8 -- in-wave phase changes by lane transposes) to spread
-// small matrices over more workgroups and waves.  At most 1024 threads and
-// 160 KiB of LDS: K = 8 wide is 1024 threads, 64 KiB plane + 4 x 20 KiB tables.
+// Two shapes per K: "wide" (8 rows per lane; 64-pack slices up to K = 6, 32
+// at K = 7 and 16 at K = 8, so that a workgroup stays at 512 threads and at
+// most 80 KiB of LDS and two of them share a CU: one's loads and stores
+// overlap the other's butterflies -- measured in profiles/r01k) for matrices
+// that fill the chip, "narrow" (16..32-pack slices, 2 rows per lane -- 4 at
+// K = 8 -- in-wave phase changes by lane transposes) to spread small matrices
+// over more workgroups and waves.
 template <int K>
 hipError_t launch_shape(bool narrow, int flags, const PassArgs &A, hipStream_t s) {
     constexpr int LRW = K < 3 ? K : 3;
-    constexpr int SPLW = K >= 8 ? 5 : 6;
+    constexpr int SPLW = K >= 8 ? 4 : K == 7 ? 5 : 6;
     if constexpr (K >= 2) {
         constexpr int LRN = K >= 8 ? 2 : 1;
         constexpr int SPLN = 6 - (K - LRN) > 4 ? 6 - (K - LRN) : 4;
@@ -716,8 +718,9 @@ __global__ void k_formal_derivative(const uint8_t *in, uint8_t *out, uint32_t ro
 }  // namespace
 
 hipError_t launch_pass(int K, int flags, const PassArgs &A, hipStream_t s) {
-    // narrow slices when 64-pack slices leave the chip under-filled
-    const uint64_t wide_groups = uint64_t(A.nsets) * ((A.packs + 63) / 64) * A.grid_chunks;
+    // narrow slices when the wide shape's slices leave the chip under-filled
+    const uint32_t wide_packs = K >= 8 ? 16 : K == 7 ? 32 : 64;
+    const uint64_t wide_groups = uint64_t(A.nsets) * ((A.packs + wide_packs - 1) / wide_packs) * A.grid_chunks;
     const bool narrow = wide_groups < 1024;
     switch (K) {
         case 0: return launch_shape<0>(narrow, flags, A, s);

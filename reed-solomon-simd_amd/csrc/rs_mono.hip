@@ -575,38 +575,50 @@ __device__ __forceinline__ void issue_col(const MonoArgs &A, uint32_t chunk, uin
     });
 }
 
-// SCALE (decode): erased rows become zero, received rows are multiplied by
-// exp(log factor) (rate_high.rs:213-231); rowinfo is indexed by work row.
-template <int L, int LR, bool SCALE>
-__device__ __forceinline__ void finish_col(const MonoArgs &A, const uint32_t *rowinfo, uint32_t (&w)[2 << LR],
-                                           Col<L, LR> &c, uint32_t lane, uint32_t wave) {
+// Decode scaling (rate_high.rs:213-231): received rows are multiplied by
+// exp(log factor), erased rows become zero; rowinfo is indexed by work row.
+// scale_issue requests the multiply tables, finish_col applies them.
+template <int L, int LR>
+struct ScaleTabs {
+    uint32_t t[1 << LR][20];
+    uint32_t erased;  // bit i: register i's row is not received
+};
+template <int L, int LR>
+__device__ __forceinline__ void scale_issue(const MonoArgs &A, const uint32_t *rowinfo, ScaleTabs<L, LR> &st,
+                                            uint32_t lane, uint32_t wave) {
     using S = SeqOf<L, LR, false>;
+    const uint32_t a = lane_rows<S, 0>(lane, wave);
+    st.erased = 0;
+    static_for<0, (1 << LR)>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const uint32_t f = rowinfo[a | reg_rows<S, 0, LR>(i)];
+        // rows that are not received read one shared dummy table (log 0):
+        // the gather costs cache lines only for the rows that use it
+        const uint32_t lg = (f & 0x10000u) ? 0u : (f & 0xFFFFu);
+        st.erased |= ((f >> 16) & 1u) << i;
+        const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + lg * 5u;
+#pragma unroll
+        for (int v = 0; v < 5; ++v) {
+            const uint4 x = q[v];
+            st.t[i][4 * v] = x.x, st.t[i][4 * v + 1] = x.y, st.t[i][4 * v + 2] = x.z, st.t[i][4 * v + 3] = x.w;
+        }
+    });
+}
+
+template <int L, int LR, bool SCALE>
+__device__ __forceinline__ void finish_col(uint32_t (&w)[2 << LR], const ScaleTabs<L, LR> *st, Col<L, LR> &c,
+                                           uint32_t lane) {
     constexpr int R = 1 << LR;
     static_for<0, R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         xpose<0>(w[2 * i], w[2 * i + 1], lane);
         c.lo[i] = w[2 * i];
         c.hi[i] = w[2 * i + 1];
+        if constexpr (SCALE) {
+            gf_mul4(c.lo[i], c.hi[i], st->t[i]);
+            if ((st->erased >> i) & 1u) c.lo[i] = c.hi[i] = 0;
+        }
     });
-    if constexpr (SCALE) {
-        const uint32_t a = lane_rows<S, 0>(lane, wave);
-        static_for<0, R>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            const uint32_t f = rowinfo[a | reg_rows<S, 0, LR>(i)];
-            // rows that are not received read one shared dummy table (log 0):
-            // the gather costs cache lines only for the rows that use it
-            const uint32_t lg = (f & 0x10000u) ? 0u : (f & 0xFFFFu);
-            uint32_t t[20];
-            const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + lg * 5u;
-#pragma unroll
-            for (int v = 0; v < 5; ++v) {
-                const uint4 x = q[v];
-                t[4 * v] = x.x, t[4 * v + 1] = x.y, t[4 * v + 2] = x.z, t[4 * v + 3] = x.w;
-            }
-            gf_mul4(c.lo[i], c.hi[i], t);
-            if (f & 0x10000u) c.lo[i] = c.hi[i] = 0;
-        });
-    }
 }
 
 template <int L, int LR, bool SCALE>
@@ -614,7 +626,9 @@ __device__ __forceinline__ void load_col(const MonoArgs &A, uint32_t chunk, uint
                                          uint32_t lane, uint32_t wave) {
     uint32_t w[2 << LR];
     issue_col<L, LR>(A, chunk, pk_off, w, lane, wave);
-    finish_col<L, LR, SCALE>(A, A.rowinfo, w, c, lane, wave);
+    ScaleTabs<L, LR> st;
+    if constexpr (SCALE) scale_issue<L, LR>(A, A.rowinfo, st, lane, wave);
+    finish_col<L, LR, SCALE>(w, &st, c, lane);
 }
 
 // Store transform rows `chunk * n + row` that fall in A.dst (placement: end
@@ -890,6 +904,10 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
     uint32_t *plane = lds;
     // XCD-aware: workgroup b runs on XCD b % 8, so the 8 packs of one 64-byte
     // block (which share cache lines) go to one XCD's L2.
+#ifdef RS_MONO_STAMPS  // entry time, before the first kernel-argument load
+    if (threadIdx.x == blockDim.x - 64 && blockIdx.x < 4096) g_mono_stamps[blockIdx.x][7] = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_mono_stamps[blockIdx.x][12] = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t b = blockIdx.x;
     const uint32_t pk = (b & 7u) * A.packs_per_xcd + (b >> 3);
     if (pk >= A.packs) return;
@@ -950,6 +968,8 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             ri = rinfo;
             RS_MSTAMP(2);
         }
+        ScaleTabs<L, LR> st;
+        if constexpr (DEC) scale_issue<L, LR>(A, ri, st, lane, wave);
 #ifndef RS_MONO_SKIP_STAGE
         static_for<0, KP1>([&](auto kc) {
             const uint32_t q = lane + 64u * decltype(kc)::value;
@@ -961,7 +981,7 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
         });
 #endif
         RS_MSTAMP(6);
-        finish_col<L, LR, DEC>(A, ri, w, c, lane, wave);
+        finish_col<L, LR, DEC>(w, &st, c, lane);
         RS_MSTAMP(1);
         const LdsTabs<L, LR> ts{priv, shared, img_i, img_f};
         // phase-3 tables: requested when phase 1 ends, written over this wave's

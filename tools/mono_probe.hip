@@ -126,10 +126,10 @@ int main(int argc, char **argv) {
     std::vector<uint64_t> st(4096 * 16);
     CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(rs::g_mono_stamps), st.size() * 8));
     uint64_t t0 = ~0ull;
-    for (uint32_t w = 0; w < wgs; ++w) t0 = std::min(t0, st[w * 16]);
-    const char *names[16] = {"start", "loaded", "eval done", "ifft A done", "remap1 done", "ifft B done", "staged", "",
-                             "fft B done", "remap2 done", "fft C done", "stored"};
-    const int order[] = {0, 2, 6, 1, 3, 4, 5, 8, 9, 10, 11};
+    for (uint32_t w = 0; w < wgs; ++w) t0 = std::min(t0, st[w * 16 + 12]);
+    const char *names[16] = {"start", "loaded", "eval done", "ifft A done", "remap1 done", "ifft B done", "staged", "entry",
+                             "fft B done", "remap2 done", "fft C done", "stored", "entry wave0"};
+    const int order[] = {12, 7, 0, 2, 6, 1, 3, 4, 5, 8, 9, 10, 11};
     for (int i : order) {
         std::vector<double> v;
         for (uint32_t w = 0; w < wgs; ++w) v.push_back((st[w * 16 + i] - t0) * 0.01);
