@@ -4,7 +4,7 @@
 // lookups on 3-bit fields of x.  Four elements are packed as one 32-bit word
 // of low bytes + one of high bytes (the reference's block layout,
 // src/algorithm.md:18-31), and v_perm_b32 performs 4 byte lookups into an
-// 8-entry table at once (12 v_perm + 10 field extracts + 6 v_bitop3 XOR3 per
+// 8-entry table at once (12 v_perm + 8 field extracts + 6 v_bitop3 XOR3 per
 // 4 elements).  A table is kPermWords = 20 words (gf_tables.hpp).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -29,12 +29,18 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // acc_l ^= (xl,xh)*m (low plane), acc_h ^= (high plane); t = 20-word perm table
 __device__ __forceinline__ void gf_muladd4(uint32_t &acc_l, uint32_t &acc_h, uint32_t xl, uint32_t xh,
                                            const uint32_t *__restrict__ t) {
+    // fields 1 and 2 of both planes by one 64-bit shift each (v_lshrrev_b64):
+    // the high plane's bits that enter the low word's top byte are masked off
+    uint64_t x3, x6;
+    const uint64_t x = (uint64_t(xh) << 32) | xl;
+    asm("v_lshrrev_b64 %0, 3, %1" : "=v"(x3) : "v"(x));
+    asm("v_lshrrev_b64 %0, 6, %1" : "=v"(x6) : "v"(x));
     const uint32_t l0 = xl & 0x07070707u;
-    const uint32_t l1 = (xl >> 3) & 0x07070707u;
-    const uint32_t l2 = (xl >> 6) & 0x03030303u;
+    const uint32_t l1 = uint32_t(x3) & 0x07070707u;
+    const uint32_t l2 = uint32_t(x6) & 0x03030303u;
     const uint32_t h0 = xh & 0x07070707u;
-    const uint32_t h1 = (xh >> 3) & 0x07070707u;
-    const uint32_t h2 = (xh >> 6) & 0x03030303u;
+    const uint32_t h1 = uint32_t(x3 >> 32) & 0x07070707u;
+    const uint32_t h2 = uint32_t(x6 >> 32) & 0x03030303u;
     // low output plane: words 0-4 (from low byte), 10-14 (from high byte)
     uint32_t pl = xor3(acc_l, __builtin_amdgcn_perm(t[1], t[0], l0), __builtin_amdgcn_perm(t[3], t[2], l1));
     pl = xor3(pl, __builtin_amdgcn_perm(t[4], t[4], l2), __builtin_amdgcn_perm(t[11], t[10], h0));

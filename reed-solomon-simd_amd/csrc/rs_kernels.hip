@@ -232,6 +232,45 @@ template <int K, int LR, int SPL, int PH, bool SCALE>
 __device__ __forceinline__ void load_rows(const PassArgs &A, const Ctx &c, uint32_t chunk, uint32_t (&lo)[1 << LR],
                                           uint32_t (&hi)[1 << LR]) {
     using P = Pass<K, LR, SPL>;
+    if (A.work_in && !SCALE) {
+        // work rows: the lane's rows are r0 + i * 2^(start(PH) + a), so their
+        // addresses are one 64-bit multiply-add plus a uniform step each
+        const uint32_t r0 = c.grow(P::template lrow<PH>(c.g, 0), K) + chunk * A.n;
+        const uint8_t *p0 = A.work_in + uint64_t(r0) * A.work_stride + c.pk_off;
+        const uint64_t step = A.work_stride << (P::start(PH) + c.a);
+        static_for<0, P::R>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            uint32_t l = 0, h = 0;
+            if (c.pk_ok) {
+                const uint8_t *p = p0 + step * uint64_t(i);
+                l = ld32(p);
+                h = ld32(p + 32);
+            }
+            lo[i] = l;
+            hi[i] = h;
+        });
+        return;
+    }
+    if (!A.work_in && A.nsrc == 1 && !SCALE) {  // one source matrix: the same, plus its row range
+        const RowMap &m = A.src[0];
+        const uint32_t r0 = c.grow(P::template lrow<PH>(c.g, 0), K) + chunk * A.n;
+        const uint32_t d = 1u << (P::start(PH) + c.a);
+        const uint8_t *p0 = m.base + int64_t(int32_t(r0 - m.row_begin)) * int64_t(m.stride) + c.pk_off;
+        const uint64_t step = m.stride << (P::start(PH) + c.a);
+        static_for<0, P::R>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            const uint32_t r = r0 + d * uint32_t(i);
+            uint32_t l = 0, h = 0;
+            if (c.pk_ok && r >= m.row_begin && r < m.row_end) {
+                const uint8_t *p = p0 + step * uint64_t(i);
+                l = ld32(p);
+                h = ld32(p + 32);
+            }
+            lo[i] = l;
+            hi[i] = h;
+        });
+        return;
+    }
     static_for<0, P::R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         const uint32_t r = pin<P::kUniform>(c.grow(P::template lrow<PH>(c.g, i), K) + chunk * A.n);
@@ -276,6 +315,37 @@ template <int K, int LR, int SPL, int PH, bool REVEAL>
 __device__ __forceinline__ void store_rows(const PassArgs &A, const Ctx &c, uint32_t chunk, const uint32_t *tabV,
                                            const uint32_t *rinfo, uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
     using P = Pass<K, LR, SPL>;
+    if (A.work_out) {  // work rows: addresses as in load_rows
+        const uint32_t r0 = c.grow(P::template lrow<PH>(c.g, 0), K) + chunk * A.n;
+        uint8_t *p0 = A.work_out + uint64_t(r0) * A.work_stride + c.pk_off;
+        const uint64_t step = A.work_stride << (P::start(PH) + c.a);
+        static_for<0, P::R>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            if (c.pk_ok) {
+                uint8_t *p = p0 + step * uint64_t(i);
+                st32(p, lo[i]);
+                st32(p + 32, hi[i]);
+            }
+        });
+        return;
+    }
+    if (!REVEAL) {  // destination matrix rows in [row_begin, row_end)
+        const RowMap &m = A.dst;
+        const uint32_t r0 = c.grow(P::template lrow<PH>(c.g, 0), K) + chunk * A.n;
+        const uint32_t d = 1u << (P::start(PH) + c.a);
+        uint8_t *p0 = const_cast<uint8_t *>(m.base) + int64_t(int32_t(r0 - m.row_begin)) * int64_t(m.stride) + c.pk_off;
+        const uint64_t step = m.stride << (P::start(PH) + c.a);
+        static_for<0, P::R>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            const uint32_t r = r0 + d * uint32_t(i);
+            if (c.pk_ok && r >= m.row_begin && r < m.row_end) {
+                uint8_t *p = p0 + step * uint64_t(i);
+                st32(p, lo[i]);
+                st32(p + 32, hi[i]);
+            }
+        });
+        return;
+    }
     static_for<0, P::R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         const uint32_t j = P::template lrow<PH>(c.g, i);
