@@ -13,7 +13,7 @@
 // Rows live in registers: a lane holds R = 2^LR rows; row-index bits are
 // spread over register bits, the 6 lane bits and the wave bits.  A butterfly
 // layer on row bit x needs x in a register bit; it gets there by a 2x2
-// register/lane transpose (DPP, ds_swizzle or v_permlane{16,32}_swap -- no
+// register/lane transpose (DPP or v_permlane{16,32}_swap -- no
 // LDS traffic, no barrier) or, for wave bits, by one LDS remap of the whole
 // column (twice per transform pair).  The plan (which bit sits where before
 // every op) is computed at compile time.
@@ -104,7 +104,7 @@ constexpr void layers(Seq &s, Map &m, int LR, const int *bits, int nb) {
 
 // Placement of a segment: in-wave bits [lo, lo + IW), wave bits the rest.
 // Registers take the first bits of `order`; lane bits the next ones, cheapest
-// transposes (permlane swaps: lane bits 5, 4; DPP: 0, 1, 3; swizzle: 2) first.
+// transposes (permlane swaps: lane bits 5, 4; DPP: 0, 1, 3; two DPP moves: 2) first.
 constexpr Map seg_map(int L, int LR, int lo, const int *order, int no) {
     const int IW = LR + 6;
     int pri[16] = {}, np = 0;
@@ -232,11 +232,15 @@ template <int J>
 __device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
     if constexpr (J == 0) return __builtin_amdgcn_update_dpp(0, int(v), 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
     else if constexpr (J == 1) return __builtin_amdgcn_update_dpp(0, int(v), 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
-    else if constexpr (J == 2) return __builtin_amdgcn_ds_swizzle(int(v), 0x101F);  // lane ^ 4
+    else if constexpr (J == 2)  // lane ^ 4 = row_half_mirror (lane ^ 7) of quad_perm 3,2,1,0 (lane ^ 3):
+        // two DPP moves instead of a ds_swizzle, whose lgkmcnt wait would also
+        // drain the twiddle-table LDS reads in flight
+        return __builtin_amdgcn_update_dpp(0, __builtin_amdgcn_update_dpp(0, int(v), 0x1B, 0xF, 0xF, false), 0x141, 0xF,
+                                           0xF, false);
     else return __builtin_amdgcn_update_dpp(0, int(v), 0x128, 0xF, 0xF, false);  // row_ror:8 = lane ^ 8
 }
 
-// Value of lane ^ 2^J (no LDS traffic except the J = 2 swizzle).
+// Value of lane ^ 2^J (DPP / permlane: no LDS traffic).
 template <int J>
 __device__ __forceinline__ uint32_t lane_xor(uint32_t v, uint32_t lane) {
     if constexpr (J == 4) {
