@@ -461,11 +461,12 @@ constexpr int kMonoPrefetch = RS_MONO_PF;
 // hides behind B - 1 layers of butterflies.  Requests never cross the remap:
 // the tables beyond it may not be in place yet (staged kernel).  `pre_remap`
 // runs just before the remap.
-// PRE0: the caller has already requested layer 0's tables into t0.  A wave
+// KPRE >= 0: the caller has already requested the tables of layer ordinal
+// KPRE into tpre (long before use: they come from global memory).  A wave
 // with `alive` false stops after the remap (its rows there are not needed).
-template <int L, int LR, bool FFT, int B0, bool PRE0 = false, typename TS, typename PreRemap>
+template <int L, int LR, bool FFT, int B0, int KPRE = -1, typename TS, typename PreRemap>
 __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR> &c, uint32_t *plane, uint32_t lane, uint32_t wave,
-                                        const PreRemap &pre_remap, const uint32_t (*t0)[20] = nullptr,
+                                        const PreRemap &pre_remap, const uint32_t (*tpre)[20] = nullptr,
                                         bool alive = true) {
     using S = SeqOf<L, LR, FFT>;
     constexpr int NT = (1 << LR) / 2;
@@ -479,7 +480,7 @@ __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR> &c, uint32_t *p
         constexpr int k0 = decltype(k0c)::value, k1 = decltype(k1c)::value;
         static_for<k0, (k0 + B < k1 ? k0 + B : k1)>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
-            if constexpr (!(PRE0 && k == 0))
+            if constexpr (k != KPRE)
                 load_layer_tabs<L, LR, S, layer_at(S::v, k), FFT>(ts, lane, wave, tb[k % B]);
         });
     };
@@ -502,13 +503,13 @@ __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR> &c, uint32_t *p
         } else {
             constexpr int k = layer_ordinal(S::v, I);
 #ifndef RS_MONO_SKIP_LAYERS
-            if constexpr (PRE0 && k == 0)
-                apply_layer<L, LR, S, I, !FFT>(*reinterpret_cast<const uint32_t(*)[NT][20]>(t0), c);
+            if constexpr (k == KPRE)
+                apply_layer<L, LR, S, I, !FFT>(*reinterpret_cast<const uint32_t(*)[NT][20]>(tpre), c);
             else
                 apply_layer<L, LR, S, I, !FFT>(tb[k % B], c);
 #endif
             constexpr int end = k < NL1 ? NL1 : NL;
-            if constexpr (k + B < end) {
+            if constexpr (k + B < end && k + B != KPRE) {
                 load_layer_tabs<L, LR, S, layer_at(S::v, k + B), FFT>(ts, lane, wave, tb[k % B]);
                 asm volatile("" ::: "memory");  // keep the request here, ahead of its use
             }
@@ -598,7 +599,10 @@ __device__ __forceinline__ void scale_issue(const MonoArgs &A, const uint32_t *r
         const uint32_t f = rowinfo[a | reg_rows<S, 0, LR>(i)];
         // rows that are not received read one shared dummy table (log 0):
         // the gather costs cache lines only for the rows that use it
-        const uint32_t lg = (f & 0x10000u) ? 0u : (f & 0xFFFFu);
+        uint32_t lg = (f & 0x10000u) ? 0u : (f & 0xFFFFu);
+#ifdef RS_MONO_SKIP_SCALE  // tools/mono_probe.hip ablation: one shared table
+        lg = 0;
+#endif
         st.erased |= ((f >> 16) & 1u) << i;
         const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + lg * 5u;
 #pragma unroll
@@ -1004,11 +1008,19 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             });
         };
         if constexpr (G::WB > 0) {
-            run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 == 1>(ts, c, plane, lane, wave, issue3, t0);
+            run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 0 : -1>(ts, c, plane, lane, wave, issue3, t0);
             RS_MSTAMP(5);
-            if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
+            // B0: the FFT's last layer (row bit 0) reads the image too; request
+            // its tables now, a whole FFT phase ahead of their use
+            using SF = SeqOf<L, LR, true>;
+            constexpr int NLF = num_layers(SF::v);
+            uint32_t tl[R / 2][20];
             const bool alive = !DEC || wave_stores<L, LR>(A, wave);
-            run_seq<L, LR, true, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, write3, nullptr, alive);
+            if constexpr (G::B0)  // (waves that stop early all read one table: no branch around the loads)
+                load_layer_tabs<L, LR, SF, layer_at(SF::v, NLF - 1), true>(GlobalTabs{img_f}, alive ? lane : 0u, wave,
+                                                                             tl);
+            if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
+            run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1>(ts, c, plane, lane, wave, write3, tl, alive);
             if (!alive) return;
         } else {
             run_seq<L, LR, false, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, NoHook{});
