@@ -26,4 +26,12 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d "$OUT/pmc_fetch" -o run
   > "$OUT/pmc_fetch.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d "$OUT/pmc_write" -o run -- python3 $BENCH \
   > "$OUT/pmc_write.log" 2>&1
+if [ "${CONFIGS:-0}" = "1" ]; then  # the other single-GPU BASELINE configs
+  timeout -k 10 300 python -u bench.py --no-cpu --config 32768x32768x1k --steps 50 --warmup 5 \
+    > "$OUT/bench_config3.json" 2>> "$OUT/bench.err"
+  timeout -k 10 300 python -u bench.py --no-cpu --config 8192x8192x64k --steps 10 --warmup 2 \
+    > "$OUT/bench_config4.json" 2>> "$OUT/bench.err"
+  timeout -k 10 300 python -u bench.py --config 32768x32768x64k --steps 10 --warmup 2 \
+    > "$OUT/bench_config5_n1.json" 2>> "$OUT/bench.err"
+fi
 echo "gpu_round $TAG done"

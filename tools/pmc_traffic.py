@@ -41,8 +41,9 @@ def main(tag):
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
-    if os.path.exists(os.path.join(src, "bench.json")):
-        shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, "bench.json"))
+    for f in ("bench.json", "bench_config3.json", "bench_config4.json", "bench_config5_n1.json"):
+        if os.path.exists(os.path.join(src, f)) and os.path.getsize(os.path.join(src, f)):
+            shutil.copy(os.path.join(src, f), os.path.join(dst, f))
     fetch = counter_means(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = counter_means(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     out = {}
