@@ -65,6 +65,7 @@ def parse():
     p.add_argument("--no-decode", action="store_true")
     p.add_argument("--no-host", action="store_true", help="skip the host-memory end-to-end measurement")
     p.add_argument("--profile-steps", type=int, default=50)
+    p.add_argument("--batch", type=int, default=64, help="stripes per call of the batched measurement (1 = skip)")
     return p.parse_args()
 
 
@@ -182,10 +183,34 @@ def main():
             def dec(op=op, rp=rp):
                 rs.decode_device(N, M, S, d_orig, op, d_rec, rp, d_out, stream=stream, ctx=ctx)
 
-            w, g = timed(dec, args.steps, args.warmup)
+            w, gt = timed(dec, args.steps, args.warmup)
             decode[f"{pct}pct"] = round(step_bytes * args.steps * world / w / 2**30, 3)
             decode[f"{pct}pct_us_per_step"] = {"wall": round(w / args.steps * 1e6, 2),
-                                               "gpu_events": round(g / args.steps * 1e6, 2)}
+                                               "gpu_events": round(gt / args.steps * 1e6, 2)}
+
+    # ---- a batch of stripes of the same shape per launch (MI355X extension:
+    # rs_encode_device_batch / rs_decode_device_batch; one erasure pattern) ----
+    batched = None
+    if args.batch > 1 and N * S * args.batch <= (1 << 31):
+        B = args.batch
+        b_orig = torch.randint(0, 256, (B, N, S), dtype=torch.uint8, device=dev, generator=g)
+        b_rec = torch.empty((B, M, S), dtype=torch.uint8, device=dev)
+        b_out = torch.empty((B, N, S), dtype=torch.uint8, device=dev)
+        bsteps = max(5, args.steps // 10)
+        w_e, g_e = timed(lambda: rs.encode_device_batch(N, M, S, b_orig, b_rec, stream=stream, ctx=ctx), bsteps,
+                         max(2, args.warmup // 5))
+        L1 = -(-min(N, M) // 100)
+        op1 = rs.present_mask([1] * (N - L1) + [0] * L1)
+        rp1 = rs.present_mask([1] * L1 + [0] * (M - L1))
+        w_d, _ = timed(lambda: rs.decode_device_batch(N, M, S, b_orig, op1, b_rec, rp1, b_out, stream=stream,
+                                                      ctx=ctx), bsteps, max(2, args.warmup // 5))
+        bbytes = step_bytes * B * world * bsteps
+        batched = {"stripes": B, "encode_GiBps": round(bbytes / w_e / 2**30, 3),
+                   "encode_us_per_launch": round(g_e / bsteps * 1e6, 2),
+                   "encode_hbm_frac": round(step_bytes * B / (g_e / bsteps) / 1e9 / HBM_PEAK_GBS, 4),
+                   "decode_1pct_GiBps": round(bbytes / w_d / 2**30, 3),
+                   "note": "B stripes of the workload's shape per call (one column-kernel launch); not the headline"}
+        del b_orig, b_rec, b_out
 
     # ---- host-memory end to end (pinned buffers, PCIe both ways) -------------
     host_e2e = None
@@ -233,6 +258,7 @@ def main():
                        "parallelism": f"replicas x{world} (independent stripes)"},
             "gpu_event_ms_per_step": round(gpu_t / args.steps * 1e3, 5),
             "decode_GiBps": decode,
+            "batched": batched,
             "host_e2e": host_e2e,
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -29,7 +29,8 @@
  *
  * Device-resident batch entry points (the performance path; no reference
  * counterpart because the reference engine only sees host slices):
- *   rs_encode_device / rs_decode_device
+ *   rs_encode_device / rs_decode_device (+ _strided, + _batch: many
+ *   stripes of one shape in one launch)
  *
  * Thread-safety: a context may be shared by threads (like DefaultEngine:
  * Send + Sync, src/lib.rs:385-409); an encoder/decoder handle is used by one
@@ -174,6 +175,27 @@ rs_status rs_decode_device_strided(rs_context *ctx, rs_rate rate, uint64_t origi
                                    const uint8_t *original_present, const void *d_recovery, uint64_t recovery_stride,
                                    const uint8_t *recovery_present, void *d_restored, uint64_t restored_stride,
                                    void *stream, rs_error *err);
+/* A batch of `stripes` independent stripes of one shape (MI355X extension: a
+ * storage node codes many stripes at once).  Stripe b's original matrix starts
+ * at d_original + b * original_stripe_stride bytes (0 = original_count rows of
+ * the row stride), likewise for the recovery / restored matrices; row strides
+ * as in the _strided calls.  Where one stripe runs as a single column-kernel
+ * launch the whole batch is one launch (stripes x shard_bytes / 8 workgroups);
+ * otherwise the stripes run one after another.  Result: identical to
+ * `stripes` separate calls.  The decode applies ONE erasure pattern to every
+ * stripe (a failed device loses the same shard indices in all of them). */
+rs_status rs_encode_device_batch(rs_context *ctx, rs_rate rate, uint64_t original_count, uint64_t recovery_count,
+                                 uint64_t shard_bytes, uint64_t stripes, const void *d_original,
+                                 uint64_t original_stride, uint64_t original_stripe_stride, void *d_recovery,
+                                 uint64_t recovery_stride, uint64_t recovery_stripe_stride, void *stream,
+                                 rs_error *err);
+rs_status rs_decode_device_batch(rs_context *ctx, rs_rate rate, uint64_t original_count, uint64_t recovery_count,
+                                 uint64_t shard_bytes, uint64_t stripes, const void *d_original,
+                                 uint64_t original_stride, uint64_t original_stripe_stride,
+                                 const uint8_t *original_present, const void *d_recovery, uint64_t recovery_stride,
+                                 uint64_t recovery_stripe_stride, const uint8_t *recovery_present, void *d_restored,
+                                 uint64_t restored_stride, uint64_t restored_stripe_stride, void *stream,
+                                 rs_error *err);
 
 /* ---- host-memory pipeline (shards arrive from a socket or file) ----
  * h_original (original_count x shard_bytes) and h_recovery (recovery_count x

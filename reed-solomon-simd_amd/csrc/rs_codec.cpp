@@ -186,6 +186,10 @@ struct Geom {
     uint64_t stride;
     uint32_t packs;
     uint64_t orig_stride = 0, rec_stride = 0, out_stride = 0;
+    // a batch of stripes of this shape: stripe b's matrices start b * *_bstride
+    // bytes after the base pointers (rs_encode_device_batch / rs_decode_device_batch)
+    uint32_t stripes = 1;
+    uint64_t orig_bstride = 0, rec_bstride = 0, out_bstride = 0;
     uint64_t orig() const { return orig_stride ? orig_stride : stride; }
     uint64_t rec() const { return rec_stride ? rec_stride : stride; }
     uint64_t out() const { return out_stride ? out_stride : stride; }
@@ -310,6 +314,7 @@ rs::MonoArgs mono_args(rs_context *ctx, uint32_t L, const Geom &g) {
     rs::MonoArgs M;
     M.packs = g.packs;
     M.packs_per_xcd = (g.packs + 7) / 8;
+    M.stripes = g.stripes;  // a batch of stripes runs in one launch
     M.img = mono_images(ctx, L);
     M.img_words = uint64_t((1u << L) - 1) * rs::kPermWords;
     M.lut = ctx->d_lut;
@@ -335,6 +340,13 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
                  uint8_t *rec, hipStream_t s) {
     const uint32_t n = uint32_t(next_pow2(M)), L = ilog2(n);
     const uint32_t C = uint32_t((N + n - 1) / n);
+    if (g.stripes > 1 && !(use_mono(ctx, L, g, C) && rs::mono_staged(int(L), C))) {  // batch: one stripe after another
+        Geom g1 = g;
+        g1.stripes = 1;
+        for (uint32_t b = 0; b < g.stripes; ++b)
+            encode_high(ctx, ws, g1, N, M, orig + b * g.orig_bstride, rec + b * g.rec_bstride, s);
+        return;
+    }
     const Levels lv = levels(L, max_k_enc(g.packs));
     rs::PassArgs A = base_args(ctx, g, n);
     A.ifft_delta = n;
@@ -343,13 +355,15 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
     if (use_mono(ctx, L, g, C)) {
         rs::MonoArgs Mo = mono_args(ctx, L, g);
         Mo.src[0] = src;
+        Mo.src_bstride[0] = g.orig_bstride;
         Mo.nsrc = 1;
         Mo.dst = dst;
+        Mo.dst_bstride = g.rec_bstride;
         Mo.chunks = C;
         Mo.ifft_img = 1;  // chunk c: skew offset c * n + n
         Mo.ifft_img_step = 1;
         Mo.fft_img = 0;
-        launch_mono(rs::kMonoEncodeHigh, L, Mo, s, (N + M) * uint64_t(g.packs) * 8);
+        launch_mono(rs::kMonoEncodeHigh, L, Mo, s, (N + M) * uint64_t(g.packs) * 8 * g.stripes);
         return;
     }
     if (lv.m == 1) {
@@ -390,6 +404,13 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
                 uint8_t *rec, hipStream_t s) {
     const uint32_t n = uint32_t(next_pow2(N)), L = ilog2(n);
     const uint32_t C = uint32_t((M + n - 1) / n);
+    if (g.stripes > 1 && !(use_mono(ctx, L, g, C) && rs::mono_staged(int(L), C))) {  // batch: one stripe after another
+        Geom g1 = g;
+        g1.stripes = 1;
+        for (uint32_t b = 0; b < g.stripes; ++b)
+            encode_low(ctx, ws, g1, N, M, orig + b * g.orig_bstride, rec + b * g.rec_bstride, s);
+        return;
+    }
     const Levels lv = levels(L, max_k_enc(g.packs));
     rs::PassArgs A = base_args(ctx, g, n);
     A.fft_delta = n;
@@ -398,13 +419,15 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
     if (use_mono(ctx, L, g, C)) {
         rs::MonoArgs Mo = mono_args(ctx, L, g);
         Mo.src[0] = src;
+        Mo.src_bstride[0] = g.orig_bstride;
         Mo.nsrc = 1;
         Mo.dst = dst;
+        Mo.dst_bstride = g.rec_bstride;
         Mo.chunks = C;
         Mo.ifft_img = 0;
         Mo.fft_img = 1;  // output chunk c: skew offset c * n + n
         Mo.fft_img_step = 1;
-        launch_mono(rs::kMonoEncodeLow, L, Mo, s, (N + M) * uint64_t(g.packs) * 8);
+        launch_mono(rs::kMonoEncodeLow, L, Mo, s, (N + M) * uint64_t(g.packs) * 8 * g.stripes);
         return;
     }
     if (lv.m == 1) {
@@ -471,13 +494,25 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
     const rs::RowMap orig_map{orig, g.orig(), high ? chunk : 0u, high ? end : uint32_t(N)};
     const rs::RowMap out_map{restored, g.out(), orig_map.row_begin, orig_map.row_end};
     const bool mono = use_mono(ctx, u, g, 1);
-    if (mono && rs::mono_staged(int(u), 1) && nd <= rs::kMonoFusedRows) {
+    const bool fused = mono && rs::mono_staged(int(u), 1) && nd <= rs::kMonoFusedRows;
+    if (g.stripes > 1 && !fused) {  // batch: one stripe after another
+        Geom g1 = g;
+        g1.stripes = 1;
+        for (uint32_t b = 0; b < g.stripes; ++b)
+            decode_dev(ctx, ws, high, g1, N, M, orig + b * g.orig_bstride, orig_present, rec + b * g.rec_bstride,
+                       rec_present, restored + b * g.out_bstride, s);
+        return;
+    }
+    if (fused) {
         // one launch: every column workgroup evaluates eval_poly itself
         rs::MonoArgs Mo = mono_args(ctx, u, g);
         Mo.src[0] = rec_map;
+        Mo.src_bstride[0] = g.rec_bstride;
         Mo.src[1] = orig_map;
+        Mo.src_bstride[1] = g.orig_bstride;
         Mo.nsrc = 2;
         Mo.dst = out_map;
+        Mo.dst_bstride = g.out_bstride;
         Mo.fused_eval = 1;
         Mo.low_rate = high ? 0 : 1;
         Mo.end = end;
@@ -487,7 +522,7 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
             Mo.erased[r >> 5] |= uint32_t(st[r] == 1) << (r & 31);
             Mo.received[r >> 5] |= uint32_t(st[r] == 2) << (r & 31);
         }
-        launch_mono(rs::kMonoDecode, u, Mo, s, (received + missing) * uint64_t(g.packs) * 8);
+        launch_mono(rs::kMonoDecode, u, Mo, s, (received + missing) * uint64_t(g.packs) * 8 * g.stripes);
         return;
     }
     uint32_t *d_rowinfo = static_cast<uint32_t *>(ws.rowinfo.get(size_t(nd) * 4));
@@ -795,6 +830,34 @@ rs_status rs_encode_device(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M
     return rs_encode_device_strided(ctx, rate, N, M, S, d_orig, 0, d_rec, 0, stream, err);
 }
 
+rs_status rs_encode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, uint64_t stripes,
+                                 const void *d_orig, uint64_t orig_stride, uint64_t orig_stripe_stride, void *d_rec,
+                                 uint64_t rec_stride, uint64_t rec_stripe_stride, void *stream, rs_error *err) {
+    if (!ctx || !ptr_ok(d_orig) || !ptr_ok(d_rec) || stripes > 0xFFFFFFFFu) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    const int high = resolve(rate, N, M, S, err);
+    if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
+    if (S % 64 || !stride_ok(orig_stride, S) || !stride_ok(rec_stride, S)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    const uint64_t orig_b = orig_stripe_stride ? orig_stripe_stride : N * (orig_stride ? orig_stride : S);
+    const uint64_t rec_b = rec_stripe_stride ? rec_stripe_stride : M * (rec_stride ? rec_stride : S);
+    if (stripes == 0) return set_err(err, RS_OK);
+    return guarded(err, [&]() -> rs_status {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        ProfScope prof(ctx);
+        Geom g{S, uint32_t(S / 8)};
+        g.orig_stride = orig_stride;
+        g.rec_stride = rec_stride;
+        g.stripes = uint32_t(stripes);
+        g.orig_bstride = orig_b;
+        g.rec_bstride = rec_b;
+        auto s = static_cast<hipStream_t>(stream);
+        if (high)
+            encode_high(ctx, ctx->ws, g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
+        else
+            encode_low(ctx, ctx->ws, g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
+        return set_err(err, RS_OK);
+    });
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------
@@ -975,6 +1038,46 @@ rs_status rs_decode_device(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M
                            void *d_restored, void *stream, rs_error *err) {
     return rs_decode_device_strided(ctx, rate, N, M, S, d_orig, 0, orig_present, d_rec, 0, rec_present, d_restored,
                                     0, stream, err);
+}
+
+rs_status rs_decode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, uint64_t stripes,
+                                 const void *d_orig, uint64_t orig_stride, uint64_t orig_stripe_stride,
+                                 const uint8_t *orig_present, const void *d_rec, uint64_t rec_stride,
+                                 uint64_t rec_stripe_stride, const uint8_t *rec_present, void *d_restored,
+                                 uint64_t restored_stride, uint64_t restored_stripe_stride, void *stream,
+                                 rs_error *err) {
+    if (!ctx || !ptr_ok(d_orig) || !ptr_ok(d_rec) || !ptr_ok(d_restored) || !orig_present || !rec_present ||
+        stripes > 0xFFFFFFFFu)
+        return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    const int high = resolve(rate, N, M, S, err);
+    if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
+    if (S % 64 || !stride_ok(orig_stride, S) || !stride_ok(rec_stride, S) || !stride_ok(restored_stride, S))
+        return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    uint64_t have_o = 0, have_r = 0;
+    for (uint64_t i = 0; i < N; ++i) have_o += orig_present[i] != 0;
+    for (uint64_t i = 0; i < M; ++i) have_r += rec_present[i] != 0;
+    if (have_o + have_r < N) {
+        set_err(err, RS_ERR_NOT_ENOUGH_SHARDS);
+        if (err) err->original_count = N, err->original_received_count = have_o, err->recovery_received_count = have_r;
+        return RS_ERR_NOT_ENOUGH_SHARDS;
+    }
+    if (have_o == N || stripes == 0) return set_err(err, RS_OK);
+    return guarded(err, [&]() -> rs_status {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        ProfScope prof(ctx);
+        Geom g{S, uint32_t(S / 8)};
+        g.orig_stride = orig_stride;
+        g.rec_stride = rec_stride;
+        g.out_stride = restored_stride;
+        g.stripes = uint32_t(stripes);
+        g.orig_bstride = orig_stripe_stride ? orig_stripe_stride : N * g.orig();
+        g.rec_bstride = rec_stripe_stride ? rec_stripe_stride : M * g.rec();
+        g.out_bstride = restored_stripe_stride ? restored_stripe_stride : N * g.out();
+        decode_dev(ctx, ctx->ws, high, g, N, M, static_cast<const uint8_t *>(d_orig), orig_present,
+                   static_cast<const uint8_t *>(d_rec), rec_present, static_cast<uint8_t *>(d_restored),
+                   static_cast<hipStream_t>(stream));
+        return set_err(err, RS_OK);
+    });
 }
 
 // ---- encoder ----------------------------------------------------------------

@@ -96,11 +96,17 @@ struct MonoArgs {
     uint32_t fused_eval = 0, low_rate = 0, end = 0, lw0 = 0;
     const uint16_t *lw_fold = nullptr;
     uint32_t erased[kMonoFusedRows / 32] = {}, received[kMonoFusedRows / 32] = {};
+    // a batch of stripes of one shape in one launch (staged kernel, grid.y =
+    // stripes): stripe b's rows sit b * *_bstride bytes after the base
+    // pointers.  Last in the struct and read only by the batch instantiation,
+    // so the single-stripe kernel's argument loads stay as they were.
+    uint32_t stripes = 1;
+    uint64_t src_bstride[2] = {0, 0}, dst_bstride = 0;
 };
 // hipErrorNotSupported: no column kernel for this L (7 <= L <= 12 are built).
 hipError_t launch_mono(int mode, int L, const MonoArgs &A, hipStream_t stream);
 // Variant launch_mono picks: LDS-staged twiddles (single chunk, 2 rows per
-// lane, L <= 11); fused_eval requires it.
+// lane, L <= 11); fused_eval and stripes > 1 require it.
 bool mono_staged(int L, uint32_t chunks);
 int mono_rows_log2_per_lane(int L, uint32_t chunks);
 

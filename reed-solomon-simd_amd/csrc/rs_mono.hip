@@ -537,12 +537,21 @@ struct NoHook {
     __device__ __forceinline__ void operator()() const {}
 };
 
-__device__ __forceinline__ const uint8_t *row_ptr(const MonoArgs &A, uint32_t r) {
+// Base pointers of this workgroup's stripe (wave-uniform, computed once).
+struct StripeBases {
+    const uint8_t *src0, *src1;
+    uint8_t *dst;
+};
+__device__ __forceinline__ StripeBases stripe_bases(const MonoArgs &A, uint32_t stripe) {
+    return {A.src[0].base + uint64_t(stripe) * A.src_bstride[0], A.src[1].base + uint64_t(stripe) * A.src_bstride[1],
+            const_cast<uint8_t *>(A.dst.base) + uint64_t(stripe) * A.dst_bstride};
+}
+
+__device__ __forceinline__ const uint8_t *row_ptr(const MonoArgs &A, const StripeBases &sb, uint32_t r) {
     const uint8_t *p = nullptr;
-    if (r >= A.src[0].row_begin && r < A.src[0].row_end)
-        p = A.src[0].base + uint64_t(r - A.src[0].row_begin) * A.src[0].stride;
+    if (r >= A.src[0].row_begin && r < A.src[0].row_end) p = sb.src0 + uint64_t(r - A.src[0].row_begin) * A.src[0].stride;
     if (A.nsrc > 1 && r >= A.src[1].row_begin && r < A.src[1].row_end)
-        p = A.src[1].base + uint64_t(r - A.src[1].row_begin) * A.src[1].stride;
+        p = sb.src1 + uint64_t(r - A.src[1].row_begin) * A.src[1].stride;
     return p;
 }
 
@@ -561,7 +570,7 @@ __device__ __forceinline__ uint32_t paired_row(uint32_t lane, uint32_t wave, int
 // paired words; finish_col completes them.  Missing rows inside the caller's
 // matrices are read and discarded by the decode's scaling.
 template <int L, int LR>
-__device__ __forceinline__ void issue_col(const MonoArgs &A, uint32_t chunk, uint32_t pk_off,
+__device__ __forceinline__ void issue_col(const MonoArgs &A, uint32_t chunk, uint32_t pk_off, const StripeBases &sb,
                                           uint32_t (&w)[2 << LR], uint32_t lane, uint32_t wave) {
     using S = SeqOf<L, LR, false>;
     const uint32_t base = chunk * (1u << L);
@@ -569,7 +578,7 @@ __device__ __forceinline__ void issue_col(const MonoArgs &A, uint32_t chunk, uin
     static_for<0, (2 << LR)>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         const uint32_t r = paired_row<S, 0, LR>(lane, wave, j) + base;
-        const uint8_t *p = row_ptr(A, r);
+        const uint8_t *p = row_ptr(A, sb, r);
         uint32_t v = 0;
 #ifdef RS_MONO_SKIP_IO
         p = nullptr;
@@ -630,10 +639,10 @@ __device__ __forceinline__ void finish_col(uint32_t (&w)[2 << LR], const ScaleTa
 }
 
 template <int L, int LR, bool SCALE>
-__device__ __forceinline__ void load_col(const MonoArgs &A, uint32_t chunk, uint32_t pk_off, Col<L, LR> &c,
-                                         uint32_t lane, uint32_t wave) {
+__device__ __forceinline__ void load_col(const MonoArgs &A, uint32_t chunk, uint32_t pk_off, const StripeBases &sb,
+                                         Col<L, LR> &c, uint32_t lane, uint32_t wave) {
     uint32_t w[2 << LR];
-    issue_col<L, LR>(A, chunk, pk_off, w, lane, wave);
+    issue_col<L, LR>(A, chunk, pk_off, sb, w, lane, wave);
     ScaleTabs<L, LR> st;
     if constexpr (SCALE) scale_issue<L, LR>(A, A.rowinfo, st, lane, wave);
     finish_col<L, LR, SCALE>(w, &st, c, lane);
@@ -644,7 +653,8 @@ __device__ __forceinline__ void load_col(const MonoArgs &A, uint32_t chunk, uint
 // multiplied by exp(65535 - log factor) (rate_high.rs:241-245).
 template <int L, int LR, bool REVEAL>
 __device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *rowinfo, uint32_t chunk,
-                                          uint32_t pk_off, Col<L, LR> &c, uint32_t lane, uint32_t wave) {
+                                          uint32_t pk_off, const StripeBases &sb, Col<L, LR> &c, uint32_t lane,
+                                          uint32_t wave) {
     using S = SeqOf<L, LR, true>;
     constexpr int I = S::v.count;
     constexpr int R = 1 << LR;
@@ -687,7 +697,7 @@ __device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *row
             keep = w[j] == 0x12345678u;
 #endif
             if (keep) {
-                uint8_t *p = const_cast<uint8_t *>(A.dst.base) + uint64_t(r - A.dst.row_begin) * A.dst.stride;
+                uint8_t *p = sb.dst + uint64_t(r - A.dst.row_begin) * A.dst.stride;
                 *reinterpret_cast<uint32_t *>(p + pk_off + half) = w[j];
             }
         }
@@ -902,7 +912,7 @@ __device__ __forceinline__ uint4 shared_piece(const uint32_t *img_i, const uint3
 #define RS_MONO_LDS_PF 2
 #endif
 
-template <int L, int LR, int MODE, bool STAGED>
+template <int L, int LR, int MODE, bool STAGED, bool BATCH>
 __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
     using C = Col<L, LR>;
     using G = Stage<L, LR>;
@@ -919,6 +929,8 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
     const uint32_t b = blockIdx.x;
     const uint32_t pk = (b & 7u) * A.packs_per_xcd + (b >> 3);
     if (pk >= A.packs) return;
+    const StripeBases sb = BATCH ? stripe_bases(A, blockIdx.y) : StripeBases{A.src[0].base, A.src[1].base,
+                                                                             const_cast<uint8_t *>(A.dst.base)};
     const uint32_t pk_off = (pk >> 3) * 64u + (pk & 7u) * 4u;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -947,7 +959,7 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             lw[1] = A.lw_fold[i0 + 1];
         }
         uint32_t w[2 << LR];
-        issue_col<L, LR>(A, 0, pk_off, w, lane, wave);
+        issue_col<L, LR>(A, 0, pk_off, sb, w, lane, wave);
         // B0: layer 0's tables come from the image; request them with the rows
         using SI = SeqOf<L, LR, false>;
         uint32_t t0[R / 2][20];
@@ -1030,15 +1042,15 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             run_seq<L, LR, true, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, NoHook{});
         }
         RS_MSTAMP(10);
-        store_col<L, LR, DEC>(A, ri, 0, pk_off, c, lane, wave);
+        store_col<L, LR, DEC>(A, ri, 0, pk_off, sb, c, lane, wave);
         RS_MSTAMP(11);
     } else if constexpr (MODE == kMonoEncodeHigh) {
         // rate_high.rs:44-87: recovery = FFT_0(XOR_c IFFT_{c n + n}(chunk c))
-        load_col<L, LR, false>(A, 0, pk_off, c, lane, wave);
+        load_col<L, LR, false>(A, 0, pk_off, sb, c, lane, wave);
         run_seq<L, LR, false, kMonoPrefetch>(GlobalTabs{img_i}, c, plane, lane, wave, NoHook{});
         for (uint32_t ch = 1; ch < A.chunks; ++ch) {
             C t;
-            load_col<L, LR, false>(A, ch, pk_off, t, lane, wave);
+            load_col<L, LR, false>(A, ch, pk_off, sb, t, lane, wave);
             run_seq<L, LR, false, kMonoPrefetch>(
                 GlobalTabs{img_i + uint64_t(ch) * A.ifft_img_step * A.img_words}, t, plane, lane, wave, NoHook{});
             static_for<0, R>([&](auto ic) {
@@ -1047,24 +1059,24 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             });
         }
         run_seq<L, LR, true, kMonoPrefetch>(GlobalTabs{img_f}, c, plane, lane, wave, NoHook{});
-        store_col<L, LR, false>(A, A.rowinfo, 0, pk_off, c, lane, wave);
+        store_col<L, LR, false>(A, A.rowinfo, 0, pk_off, sb, c, lane, wave);
     } else if constexpr (MODE == kMonoEncodeLow) {
         // rate_low.rs:44-87: recovery chunk c = FFT_{c n + n}(IFFT_0(original))
-        load_col<L, LR, false>(A, 0, pk_off, c, lane, wave);
+        load_col<L, LR, false>(A, 0, pk_off, sb, c, lane, wave);
         run_seq<L, LR, false, kMonoPrefetch>(GlobalTabs{img_i}, c, plane, lane, wave, NoHook{});
         for (uint32_t ch = 0; ch < A.chunks; ++ch) {
             C t = c;
             run_seq<L, LR, true, kMonoPrefetch>(
                 GlobalTabs{img_f + uint64_t(ch) * A.fft_img_step * A.img_words}, t, plane, lane, wave, NoHook{});
-            store_col<L, LR, false>(A, A.rowinfo, ch, pk_off, t, lane, wave);
+            store_col<L, LR, false>(A, A.rowinfo, ch, pk_off, sb, t, lane, wave);
         }
     } else {
         // rate_high.rs:213-245 / rate_low.rs:213-245 after eval_poly
-        load_col<L, LR, true>(A, 0, pk_off, c, lane, wave);
+        load_col<L, LR, true>(A, 0, pk_off, sb, c, lane, wave);
         run_seq<L, LR, false, kMonoPrefetch>(GlobalTabs{img_i}, c, plane, lane, wave, NoHook{});
         formal_derivative<L, LR>(c, plane, lane, wave);
         run_seq<L, LR, true, kMonoPrefetch>(GlobalTabs{img_f}, c, plane, lane, wave, NoHook{});
-        store_col<L, LR, true>(A, A.rowinfo, 0, pk_off, c, lane, wave);
+        store_col<L, LR, true>(A, A.rowinfo, 0, pk_off, sb, c, lane, wave);
     }
 }
 
@@ -1083,20 +1095,20 @@ constexpr int mono_lr(int L, bool staged) {
     return staged ? 1 : L <= 10 ? (RS_MONO_LR10 < L - 6 ? RS_MONO_LR10 : L - 6) : L - 9;
 }
 
-template <int L, int MODE, bool STAGED>
+template <int L, int MODE, bool STAGED, bool BATCH = false>
 hipError_t launch_ls(const MonoArgs &A, hipStream_t s) {
     constexpr int LR = mono_lr(L, STAGED);
     const size_t lds = STAGED ? size_t(MODE == kMonoDecode ? Stage<L, LR>::words_dec : Stage<L, LR>::words) * 4
                               : size_t(8) << L;
     static bool attr_set = false;  // benign race: idempotent attribute call
     if (!attr_set && lds > 65536) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mono<L, LR, MODE, STAGED>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mono<L, LR, MODE, STAGED, BATCH>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const uint32_t grid = 8u * A.packs_per_xcd;
-    k_mono<L, LR, MODE, STAGED><<<dim3(grid), 1 << (L - LR), lds, s>>>(A);
+    k_mono<L, LR, MODE, STAGED, BATCH><<<dim3(grid, BATCH ? A.stripes : 1), 1 << (L - LR), lds, s>>>(A);
     return hipGetLastError();
 }
 
@@ -1107,10 +1119,11 @@ hipError_t launch_l(const MonoArgs &A, hipStream_t s) {
     if constexpr (staged_l(L)) {
         if (A.chunks == 1) {  // = mono_staged()
             if (MODE == kMonoDecode && !A.fused_eval) return hipErrorInvalidValue;
+            if (A.stripes > 1) return launch_ls<L, MODE, true, true>(A, s);
             return launch_ls<L, MODE, true>(A, s);
         }
     }
-    if (A.fused_eval) return hipErrorInvalidValue;
+    if (A.fused_eval || A.stripes > 1) return hipErrorInvalidValue;
     return launch_ls<L, MODE, false>(A, s);
 }
 

@@ -92,6 +92,9 @@ _sig("rs_decode_device", _int, _vp, _int, _u64, _u64, _u64, _vp, ctypes.c_char_p
 _sig("rs_encode_device_strided", _int, _vp, _int, _u64, _u64, _u64, _vp, _u64, _vp, _u64, _vp, _E)
 _sig("rs_decode_device_strided", _int, _vp, _int, _u64, _u64, _u64, _vp, _u64, ctypes.c_char_p, _vp, _u64,
      ctypes.c_char_p, _vp, _u64, _vp, _E)
+_sig("rs_encode_device_batch", _int, _vp, _int, _u64, _u64, _u64, _u64, _vp, _u64, _u64, _vp, _u64, _u64, _vp, _E)
+_sig("rs_decode_device_batch", _int, _vp, _int, _u64, _u64, _u64, _u64, _vp, _u64, _u64, ctypes.c_char_p, _vp, _u64,
+     _u64, ctypes.c_char_p, _vp, _u64, _u64, _vp, _E)
 _sig("rs_engine_fft", _int, _vp, _vp, _u64, _u64, _u64, _u64, _u64, _u64, _vp)
 _sig("rs_engine_ifft", _int, _vp, _vp, _u64, _u64, _u64, _u64, _u64, _u64, _vp)
 _sig("rs_engine_mul", _int, _vp, _vp, _u64, ctypes.c_uint16, _vp)
@@ -629,6 +632,46 @@ def encode_device(original_count: int, recovery_count: int, shard_bytes: int, d_
     _raise(_lib.rs_encode_device_strided(ctx.handle, rate_, original_count, recovery_count, shard_bytes,
                                          _ptr(d_original), _row_stride(d_original), _ptr(d_recovery),
                                          _row_stride(d_recovery), _stream(stream), ctypes.byref(err)), err)
+
+
+def _batch_strides(x):
+    """(row stride, stripe stride) in bytes of a 3-D uint8 tensor [stripes, rows, shard_bytes]
+    whose rows are contiguous (0 = packed)."""
+    if x.dim() != 3 or x.stride(2) != 1:
+        raise ValueError("batch matrices must be [stripes, rows, shard_bytes] with contiguous rows")
+    return int(x.stride(1)) * x.element_size(), int(x.stride(0)) * x.element_size()
+
+
+def encode_device_batch(original_count: int, recovery_count: int, shard_bytes: int, d_original, d_recovery,
+                        stream=None, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None) -> None:
+    """Encode a batch of stripes of one shape (rs_encode_device_batch): d_original
+    [stripes, original_count, shard_bytes], d_recovery [stripes, recovery_count, shard_bytes]."""
+    ctx = ctx or default_context()
+    if d_original.shape[0] != d_recovery.shape[0]:
+        raise ValueError("original and recovery batches differ in stripe count")
+    (o_row, o_b), (r_row, r_b) = _batch_strides(d_original), _batch_strides(d_recovery)
+    err = _RsError()
+    _raise(_lib.rs_encode_device_batch(ctx.handle, rate_, original_count, recovery_count, shard_bytes,
+                                       d_original.shape[0], d_original.data_ptr(), o_row, o_b, d_recovery.data_ptr(),
+                                       r_row, r_b, _stream(stream), ctypes.byref(err)), err)
+
+
+def decode_device_batch(original_count: int, recovery_count: int, shard_bytes: int, d_original, original_present,
+                        d_recovery, recovery_present, d_restored, stream=None, rate_: int = RATE_DEFAULT,
+                        ctx: Optional[Context] = None) -> None:
+    """Decode a batch of stripes sharing ONE erasure pattern (rs_decode_device_batch); tensors
+    [stripes, rows, shard_bytes]; only missing originals of d_restored are written."""
+    ctx = ctx or default_context()
+    n = d_original.shape[0]
+    if d_recovery.shape[0] != n or d_restored.shape[0] != n:
+        raise ValueError("batches differ in stripe count")
+    (o_row, o_b), (r_row, r_b), (x_row, x_b) = (_batch_strides(d_original), _batch_strides(d_recovery),
+                                                _batch_strides(d_restored))
+    err = _RsError()
+    _raise(_lib.rs_decode_device_batch(ctx.handle, rate_, original_count, recovery_count, shard_bytes, n,
+                                       d_original.data_ptr(), o_row, o_b, present_mask(original_present),
+                                       d_recovery.data_ptr(), r_row, r_b, present_mask(recovery_present),
+                                       d_restored.data_ptr(), x_row, x_b, _stream(stream), ctypes.byref(err)), err)
 
 
 def present_mask(flags) -> bytes:

@@ -594,3 +594,63 @@ def test_host_pipeline_matches_oracle(torch, rs, rate, N, M, S, slices, pinned):
     miss = op == 0
     assert np.array_equal(h_out[miss], orig[miss])
     assert np.all(h_out[~miss] == 0x33), "present rows of the output must not be written"
+
+
+# ---------------------------------------------------------------------------
+# batches of stripes (rs_encode_device_batch / rs_decode_device_batch): every
+# stripe equals the oracle's single-stripe result.  Column-kernel shapes run
+# the batch as one launch; the others loop over the stripes.
+
+BATCH_CASES = [
+    # (rate, N, M, S, stripes)
+    ("default", 1024, 1024, 1024, 3), ("default", 1000, 1000, 576, 2), ("low", 100, 1000, 128, 3),
+    ("default", 200, 56, 2048, 4), ("default", 5000, 300, 256, 2), ("default", 64, 64, 1024, 5),
+]
+
+
+@pytest.mark.parametrize("rate,N,M,S,B", BATCH_CASES)
+def test_batch_encode_decode_match_oracle(torch, rs, rate, N, M, S, B):
+    origs = [O.generate_original(N, S, 40 + b) for b in range(B)]
+    d_o = _dev(torch, np.stack(origs))
+    # recovery rows padded to a wider stripe pitch: the stripe stride is not M rows
+    d_r_full = torch.full((B, M + 3, S), 0xEE, dtype=torch.uint8, device="cuda")
+    d_r = d_r_full[:, :M, :]
+    rs.encode_device_batch(N, M, S, d_o, d_r, rate_=RATE[rate])
+    torch.cuda.synchronize()
+    got = d_r.cpu().numpy()
+    recs = [O.encode(rate, origs[b], M) for b in range(B)]
+    for b in range(B):
+        assert np.array_equal(got[b], recs[b]), f"stripe {b}"
+    assert np.all(d_r_full[:, M:, :].cpu().numpy() == 0xEE), "padding rows must not be written"
+    # one erasure pattern for every stripe
+    rng = np.random.default_rng(N + M + B)
+    L = max(1, min(N, M) // 10)
+    op = np.ones(N, np.uint8)
+    op[rng.choice(N, L, replace=False)] = 0
+    rp = np.zeros(M, np.uint8)
+    rp[rng.choice(M, L, replace=False)] = 1
+    d_oo = _dev(torch, np.stack([np.where(op[:, None] == 1, o, 0xA5).astype(np.uint8) for o in origs]))
+    d_rr = _dev(torch, np.stack([np.where(rp[:, None] == 1, r, 0x5A).astype(np.uint8) for r in recs]))
+    d_out = torch.full((B, N, S), 0x33, dtype=torch.uint8, device="cuda")
+    rs.decode_device_batch(N, M, S, d_oo, op, d_rr, rp, d_out, rate_=RATE[rate])
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    miss = op == 0
+    for b in range(B):
+        assert np.array_equal(out[b][miss], origs[b][miss]), f"stripe {b}"
+        assert np.all(out[b][~miss] == 0x33)
+
+
+def test_batch_matches_single_stripe_calls_at_headline(torch, rs):
+    """64 stripes of the headline shape in one launch == 64 single-stripe encodes."""
+    B, N, M, S = 64, 1024, 1024, 1024
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    d_o = torch.randint(0, 256, (B, N, S), dtype=torch.uint8, device="cuda", generator=g)
+    d_r = torch.empty((B, M, S), dtype=torch.uint8, device="cuda")
+    rs.encode_device_batch(N, M, S, d_o, d_r)
+    one = torch.empty((M, S), dtype=torch.uint8, device="cuda")
+    for b in (0, 17, 63):
+        rs.encode_device(N, M, S, d_o[b], one)
+        torch.cuda.synchronize()
+        assert torch.equal(one, d_r[b]), f"stripe {b}"
