@@ -215,6 +215,7 @@ constexpr uint32_t kMaxK = 8;  // pass kernels exist for K <= 8
 // win for encodes (8192:8192 x 64 KiB 747 -> 857 GiB/s) and decodes (377 ->
 // 396 GiB/s); 8-bit passes only once a transform has thousands of packs
 // (32768:32768 x 64 KiB encode 820 -> 884 GiB/s; at 1 KiB shards 656 -> 505).
+constexpr uint64_t kMaxBatchStripes = 65535;  // stripes per column-kernel launch (grid.y)
 uint32_t g_max_k = 0;  // RS_MI355X_MAX_K (4..8) overrides the choice below
 uint32_t max_k_enc(uint32_t packs) { return g_max_k ? g_max_k : packs >= 2048 ? 8 : 7; }
 uint32_t max_k_dec() { return g_max_k ? g_max_k : 7; }
@@ -833,7 +834,7 @@ rs_status rs_encode_device(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M
 rs_status rs_encode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, uint64_t stripes,
                                  const void *d_orig, uint64_t orig_stride, uint64_t orig_stripe_stride, void *d_rec,
                                  uint64_t rec_stride, uint64_t rec_stripe_stride, void *stream, rs_error *err) {
-    if (!ctx || !ptr_ok(d_orig) || !ptr_ok(d_rec) || stripes > 0xFFFFFFFFu) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    if (!ctx || !ptr_ok(d_orig) || !ptr_ok(d_rec)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     const int high = resolve(rate, N, M, S, err);
     if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
     if (S % 64 || !stride_ok(orig_stride, S) || !stride_ok(rec_stride, S)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
@@ -846,14 +847,18 @@ rs_status rs_encode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint
         Geom g{S, uint32_t(S / 8)};
         g.orig_stride = orig_stride;
         g.rec_stride = rec_stride;
-        g.stripes = uint32_t(stripes);
         g.orig_bstride = orig_b;
         g.rec_bstride = rec_b;
         auto s = static_cast<hipStream_t>(stream);
-        if (high)
-            encode_high(ctx, ctx->ws, g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
-        else
-            encode_low(ctx, ctx->ws, g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
+        for (uint64_t b0 = 0; b0 < stripes; b0 += kMaxBatchStripes) {  // grid.y limit
+            g.stripes = uint32_t(std::min<uint64_t>(kMaxBatchStripes, stripes - b0));
+            const uint8_t *o = static_cast<const uint8_t *>(d_orig) + b0 * orig_b;
+            uint8_t *r = static_cast<uint8_t *>(d_rec) + b0 * rec_b;
+            if (high)
+                encode_high(ctx, ctx->ws, g, N, M, o, r, s);
+            else
+                encode_low(ctx, ctx->ws, g, N, M, o, r, s);
+        }
         return set_err(err, RS_OK);
     });
 }
@@ -1046,8 +1051,7 @@ rs_status rs_decode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint
                                  uint64_t rec_stripe_stride, const uint8_t *rec_present, void *d_restored,
                                  uint64_t restored_stride, uint64_t restored_stripe_stride, void *stream,
                                  rs_error *err) {
-    if (!ctx || !ptr_ok(d_orig) || !ptr_ok(d_rec) || !ptr_ok(d_restored) || !orig_present || !rec_present ||
-        stripes > 0xFFFFFFFFu)
+    if (!ctx || !ptr_ok(d_orig) || !ptr_ok(d_rec) || !ptr_ok(d_restored) || !orig_present || !rec_present)
         return set_err(err, RS_ERR_INVALID_ARGUMENT);
     const int high = resolve(rate, N, M, S, err);
     if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
@@ -1069,13 +1073,15 @@ rs_status rs_decode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint
         g.orig_stride = orig_stride;
         g.rec_stride = rec_stride;
         g.out_stride = restored_stride;
-        g.stripes = uint32_t(stripes);
         g.orig_bstride = orig_stripe_stride ? orig_stripe_stride : N * g.orig();
         g.rec_bstride = rec_stripe_stride ? rec_stripe_stride : M * g.rec();
         g.out_bstride = restored_stripe_stride ? restored_stripe_stride : N * g.out();
-        decode_dev(ctx, ctx->ws, high, g, N, M, static_cast<const uint8_t *>(d_orig), orig_present,
-                   static_cast<const uint8_t *>(d_rec), rec_present, static_cast<uint8_t *>(d_restored),
-                   static_cast<hipStream_t>(stream));
+        for (uint64_t b0 = 0; b0 < stripes; b0 += kMaxBatchStripes) {  // grid.y limit
+            g.stripes = uint32_t(std::min<uint64_t>(kMaxBatchStripes, stripes - b0));
+            decode_dev(ctx, ctx->ws, high, g, N, M, static_cast<const uint8_t *>(d_orig) + b0 * g.orig_bstride,
+                       orig_present, static_cast<const uint8_t *>(d_rec) + b0 * g.rec_bstride, rec_present,
+                       static_cast<uint8_t *>(d_restored) + b0 * g.out_bstride, static_cast<hipStream_t>(stream));
+        }
         return set_err(err, RS_OK);
     });
 }

@@ -209,3 +209,15 @@ def test_python_binding_declares_every_signature():
     for name in sorted(used):
         f = getattr(rs._lib, name)
         assert f.argtypes is not None, f"{name} has no declared argtypes"
+
+
+def test_batch_entry_points_validate_before_any_device_work(rs):
+    """rs_*_device_batch reject bad arguments like the single-stripe calls (no GPU needed)."""
+    import ctypes
+    err = rs._RsError()
+    # null context / pointers
+    assert rs._lib.rs_encode_device_batch(None, 0, 1024, 1024, 1024, 3, 0, 0, 0, 0, 0, 0, None,
+                                          ctypes.byref(err)) == 101
+    op = bytes([1] * 4)
+    assert rs._lib.rs_decode_device_batch(None, 0, 4, 4, 64, 2, 0, 0, 0, op, 0, 0, 0, op, 0, 0, 0, None,
+                                          ctypes.byref(err)) == 101
