@@ -62,6 +62,7 @@ def parse():
     p.add_argument("--config", default="1024x1024x1k", choices=sorted(CONFIGS))
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-copy", action="store_true", help="skip the 1 GiB device-copy context measurement")
     p.add_argument("--no-decode", action="store_true")
     p.add_argument("--no-host", action="store_true", help="skip the host-memory end-to-end measurement")
     p.add_argument("--profile-steps", type=int, default=50)
@@ -242,6 +243,23 @@ def main():
                     "decode_1pct_GiBps": round(world * step_bytes / ddt / 2**30, 3), "slices": best[0],
                     "note": "pinned host buffers, hipMemcpy2DAsync in + kernels + out, column slices over 3 streams"}
 
+    # ---- device copy for context (STREAM-copy GB/s) ---------
+    copy_ref = None
+    if not args.no_copy:
+        nb = 1 << 30
+        c_src = torch.empty(nb, dtype=torch.uint8, device=dev)
+        c_dst = torch.empty_like(c_src)
+        c_dst.copy_(c_src)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            c_dst.copy_(c_src)
+        e1.record()
+        torch.cuda.synchronize()
+        copy_ref = {"GBps": round(2 * nb * 10 / (e0.elapsed_time(e1) / 1e3) / 1e9, 1),
+                    "note": "torch device-to-device copy of 1 GiB (read + write bytes), context for roofline.peak"}
+        del c_src, c_dst
+
     # ---- CPU baseline (rank 0, N = 1 only) ----------------------------------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -261,6 +279,7 @@ def main():
             "batched": batched,
             "host_e2e": host_e2e,
             "roofline": roofline,
+            "device_copy": copy_ref,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
@@ -357,23 +376,48 @@ def load_traffic(kernel):
 
 
 def cpu_baseline(seconds):
-    """AVX2 restatement of the reference engine, 1 thread, 1024:1024 x 1 KiB encode."""
+    """AVX2 restatement of the reference engine (oracle/avx2_port.c), 1024:1024 x 1 KiB encode:
+    `value` on 1 thread (the reference is single-threaded); `all_cores` = independent stripes on
+    every host thread this process may use (at most 16, the GPU box's CPU share), an upper bound."""
+    import threading
+
     import numpy as np
     import oracle_lib as O
 
     if O.lib().orc_select_engine(1) != 0:
         return {"value": None, "unit": "GiB/s", "cores": 1, "kind": "port", "sample": "AVX2 unavailable on host"}
     orig = np.random.default_rng(0).integers(0, 256, (1024, 1024), dtype=np.uint8)
-    O.encode("default", orig, 1024)
+    O.encode("default", orig, 1024)  # tables built once, before any thread starts
     it, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         O.encode("default", orig, 1024)
         it += 1
     dt = time.perf_counter() - t0
+
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    counts = [0] * threads
+    stop = time.perf_counter() + max(1.0, seconds / 2)
+
+    def worker(i):  # ctypes releases the GIL; the oracle's work buffer is thread-local
+        mine = orig.copy()
+        while time.perf_counter() < stop:
+            O.encode("default", mine, 1024)
+            counts[i] += 1
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
+    t1 = time.perf_counter()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    dt_all = time.perf_counter() - t1
     O.lib().orc_select_engine(0)
+    cpu = f"{platform.processor() or platform.machine()}"
     return {"value": round(2 * 1024 * 1024 * it / dt / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"{it} encodes of 1024:1024 x 1024 B in {dt:.1f} s (shard copy-in + encode, like "
-                      f"benches/benchmarks.rs:101-107), single thread, {platform.processor() or platform.machine()}"}
+                      f"benches/benchmarks.rs:101-107), single thread, {cpu}",
+            "all_cores": {"value": round(2 * 1024 * 1024 * sum(counts) / dt_all / 2**30, 4), "cores": threads,
+                          "sample": f"{sum(counts)} independent encodes on {threads} threads in {dt_all:.1f} s"}}
 
 
 if __name__ == "__main__":

@@ -78,7 +78,7 @@ static void fwht(gf *v, uint32_t n) {
 void orc_init(void) {
     if (g_ready) return;
     /* LFSR pass: polynomial-basis element -> discrete log. */
-    static gf plog[GF_ORDER];
+    static _Thread_local gf plog[GF_ORDER];
     uint32_t st = 1;
     for (uint32_t k = 0; k < GF_MOD; k++) {
         plog[st] = (gf)k;
@@ -87,7 +87,7 @@ void orc_init(void) {
     }
     plog[0] = GF_MOD;
     /* Cantor coordinates -> polynomial element -> log. */
-    static gf poly[GF_ORDER];
+    static _Thread_local gf poly[GF_ORDER];
     poly[0] = 0;
     for (int b = 0; b < GF_BITS; b++) {
         uint32_t w = 1u << b;
@@ -266,8 +266,8 @@ static void extract_shard(const uint8_t *work, size_t blocks, size_t row, uint8_
 
 /* Work buffer re-used across calls, like the reference's EncoderWork /
  * DecoderWork (shards.rs:30-36 keeps its allocation). */
-static uint8_t *g_work = NULL;
-static size_t g_work_cap = 0;
+static _Thread_local uint8_t *g_work = NULL; /* per thread: bench.py times the CPU baseline on all cores */
+static _Thread_local size_t g_work_cap = 0;
 static uint8_t *work_buf(size_t bytes) {
     if (bytes > g_work_cap) {
         free(g_work);
