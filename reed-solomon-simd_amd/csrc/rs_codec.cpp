@@ -328,8 +328,9 @@ void launch_mono(int mode, uint32_t L, const rs::MonoArgs &M, hipStream_t s, uin
     check(rs::launch_mono(mode, int(L), M, s));
     if (t_prof_ctx) {
         static thread_local char buf[64];
-        snprintf(buf, sizeof buf, "k_mono<%u, %d, %d, %s>", L, rs::mono_rows_log2_per_lane(int(L), M.chunks), mode,
-                 rs::mono_staged(int(L), M.chunks) ? "true" : "false");
+        const bool staged = rs::mono_staged(int(L), M.chunks);  // the template's name, as rocprofv3 prints it
+        snprintf(buf, sizeof buf, "k_mono<%u, %d, %d, %s, %s>", L, rs::mono_rows_log2_per_lane(int(L), M.chunks), mode,
+                 staged ? "true" : "false", staged && M.stripes > 1 ? "true" : "false");
         prof_end(s, ev, buf, bytes);
     }
 }

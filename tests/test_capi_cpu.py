@@ -221,3 +221,15 @@ def test_batch_entry_points_validate_before_any_device_work(rs):
     op = bytes([1] * 4)
     assert rs._lib.rs_decode_device_batch(None, 0, 4, 4, 64, 2, 0, 0, 0, op, 0, 0, 0, op, 0, 0, 0, None,
                                           ctypes.byref(err)) == 101
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is present on this host")
+def test_no_cpu_fallback_without_a_gpu(rs):
+    """The product path has no CPU fallback: with no device every compute entry point
+    (one-shot API, encoder objects, device context) raises DeviceError instead of computing."""
+    with pytest.raises(rs.DeviceError):
+        rs.Context()
+    with pytest.raises(rs.DeviceError):
+        rs.encode(3, 5, [bytes(64)] * 3)
+    with pytest.raises(rs.DeviceError):
+        rs.ReedSolomonEncoder(3, 5, 64)
