@@ -465,6 +465,49 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
     }
 }
 
+// FFT passes of a multi-level decode, pruned to the rows that reach an output.
+// The last pass stores only erased originals; the pass at level k (bits
+// [lo_k, lo_k + K_k)) feeds the lower levels only within aligned superblocks
+// of 2^(lo_k + K_k) rows, and its row sets {s_lo + j 2^lo_k + s_hi 2^(lo_k+K_k)}
+// (set = s_lo + s_hi 2^lo_k) lie in superblock s_hi.  A superblock holding no
+// erased row in the restored range is not launched; the needed ones go out as
+// at most kFftRuns launches of consecutive sets (smallest gaps bridged first).
+// A pruned FFT: the reference transforms every row (rate_high.rs:241-246) and
+// reads back only the erased ones, so the restored rows are the same bytes.
+constexpr size_t kFftRuns = 4;
+void fft_pass_pruned(rs::PassArgs P, const Levels &lv, uint32_t k, uint32_t nd, const std::vector<uint8_t> &st,
+                     const rs::RowMap &out, hipStream_t s) {
+    const uint32_t a = lv.lo[k], sb_log = a + lv.K[k], nsb = nd >> sb_log;
+    std::vector<std::pair<uint32_t, uint32_t>> runs;  // [begin, end) superblocks
+    std::vector<uint64_t> erased;                      // erased rows in range per run
+    for (uint32_t sb = 0; sb < nsb; ++sb) {
+        const uint32_t r0 = std::max(sb << sb_log, out.row_begin), r1 = std::min((sb + 1) << sb_log, out.row_end);
+        uint64_t e = 0;
+        for (uint32_t r = r0; r < r1; ++r) e += st[r] == 1;
+        if (!e) continue;
+        if (!runs.empty() && runs.back().second == sb) {
+            runs.back().second = sb + 1;
+            erased.back() += e;
+        } else {
+            runs.push_back({sb, sb + 1});
+            erased.push_back(e);
+        }
+    }
+    while (runs.size() > kFftRuns) {
+        size_t j = 0;  // bridge the smallest gap: runs j and j + 1
+        for (size_t i = 1; i + 1 < runs.size(); ++i)
+            if (runs[i + 1].first - runs[i].second < runs[j + 1].first - runs[j].second) j = i;
+        runs[j].second = runs[j + 1].second;
+        erased[j] += erased[j + 1];
+        runs.erase(runs.begin() + j + 1);
+        erased.erase(erased.begin() + j + 1);
+    }
+    for (size_t i = 0; i < runs.size(); ++i) {
+        P.set_base = runs[i].first << a;
+        launch(int(lv.K[k]), rs::kFft, P, (runs[i].second - runs[i].first) << a, a, s, 0, P.reveal ? erased[i] : 0);
+    }
+}
+
 // Decode (rate_high.rs:172-254 / rate_low.rs:172-254).  Only missing original
 // rows of `restored` are written.
 //
@@ -608,7 +651,7 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
         } else {
             P.work_out = U;
         }
-        run_level(P, lv, k, rs::kFft, nd, s, 0, k == 0 ? missing : 0);
+        fft_pass_pruned(P, lv, uint32_t(k), nd, st, out_map, s);
     }
 }
 

@@ -23,7 +23,8 @@ struct RowMap {
 // the matching 4 high bytes at 32 + 4p (reference layout, algorithm.md:18-31).
 struct PassArgs {
     uint32_t a = 0;        // stride exponent of the row set
-    uint32_t nsets = 1;    // row sets per chunk (n >> K)
+    uint32_t nsets = 1;    // row sets of this launch (n >> K, fewer for a pruned reveal)
+    uint32_t set_base = 0; // first row set of this launch (pruned decode reveal passes)
     uint32_t n = 1;        // transform size (rows per chunk)
     uint32_t packs = 0;    // packs per row (shard_bytes / 8)
     uint32_t slices = 0;   // ceil(packs / 64)

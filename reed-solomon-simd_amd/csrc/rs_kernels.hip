@@ -593,7 +593,7 @@ __device__ __forceinline__ Ctx make_ctx(const PassArgs &A, uint32_t bx) {
     c.g = threadIdx.x >> SPL;
     if constexpr (P::kUniform) c.g = __builtin_amdgcn_readfirstlane(c.g);
     const uint32_t slice = bx % A.slices;
-    const uint32_t set = bx / A.slices;
+    const uint32_t set = A.set_base + bx / A.slices;
     c.a = A.a;
     c.s_lo = set & ((1u << A.a) - 1u);
     c.s_hi = set >> A.a;

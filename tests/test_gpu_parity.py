@@ -654,3 +654,52 @@ def test_batch_matches_single_stripe_calls_at_headline(torch, rs):
         rs.encode_device(N, M, S, d_o[b], one)
         torch.cuda.synchronize()
         assert torch.equal(one, d_r[b]), f"stripe {b}"
+
+
+# ---------------------------------------------------------------------------
+# pruned FFT passes (rs_codec.cpp fft_pass_pruned): below the top level, only
+# the row sets whose superblock holds erased originals are launched (at most 4
+# runs per pass); 16384:16384 and 20000:30000 (low) decode over 3 levels
+
+def _loss_pattern(kind, N, rng):
+    op = np.ones(N, np.uint8)
+    if kind == "tail":
+        op[N - max(1, N // 100):] = 0
+    elif kind == "head":
+        op[:max(1, N // 100)] = 0
+    elif kind == "middle":
+        op[N // 2 - 40:N // 2 + 41] = 0
+    elif kind == "one":
+        op[N // 3] = 0
+    elif kind == "spread":  # many runs: gaps bridged down to 4 launches
+        op[::max(1, N // 9)] = 0
+    elif kind == "random":
+        op[rng.choice(N, max(1, N // 50), replace=False)] = 0
+    elif kind == "all":
+        op[:] = 0
+    return op
+
+
+@pytest.mark.parametrize("kind", ["tail", "head", "middle", "one", "spread", "random", "all"])
+@pytest.mark.parametrize("rate,N,M,S", [("high", 4096, 4096, 128), ("low", 3000, 5000, 64),
+                                        ("high", 8192, 8192, 64), ("high", 1024, 1024, 1024),
+                                        ("high", 16384, 16384, 64), ("low", 20000, 30000, 64)])
+@pytest.mark.parametrize("mono", [1, 0])
+def test_decode_loss_patterns_pruned_reveal(torch, rs, kind, rate, N, M, S, mono):
+    rs.mono_enable(mono)
+    try:
+        orig = O.generate_original(N, S, 9)
+        rec = O.encode(rate, orig, M)
+        op = _loss_pattern(kind, N, np.random.default_rng(N + S))
+        L = int((op == 0).sum())
+        if L > M:
+            pytest.skip("more losses than recovery shards")
+        rp = np.zeros(M, np.uint8)
+        rp[np.random.default_rng(M).choice(M, L, replace=False)] = 1
+        got = gpu_decode(torch, rs, rate, orig, op, rec, rp)
+        miss = op == 0
+        assert np.array_equal(got[miss], orig[miss])
+        assert np.all(got[~miss] == 0x33), "present rows of the output must not be written"
+        rs.check_device()
+    finally:
+        rs.mono_enable(1)
