@@ -696,6 +696,52 @@ def decode_device(original_count: int, recovery_count: int, shard_bytes: int, d_
                                          _stream(stream), ctypes.byref(err)), err)
 
 
+class DeviceCall:
+    """A device encode / decode bound once to fixed shapes, buffers and stream
+    (`encode_device_call` / `decode_device_call`): each call is one C-ABI call
+    (rs_encode_device_strided / rs_decode_device_strided) with pre-converted
+    arguments, ≈1 µs of Python instead of ≈4 µs for the keyword wrappers --
+    what a storage server coding many stripes through fixed staging buffers
+    does, and what a Rust / C caller of the ABI pays (nothing).  The buffers
+    and masks are kept alive by the object."""
+
+    def __init__(self, fn, args, keep):
+        self._fn = fn
+        self._err = _RsError()
+        self._args = tuple(args) + (ctypes.byref(self._err),)
+        self._keep = keep
+
+    def __call__(self) -> None:
+        code = self._fn(*self._args)
+        if code:
+            _raise(code, self._err)
+
+
+def encode_device_call(original_count: int, recovery_count: int, shard_bytes: int, d_original, d_recovery,
+                       stream=None, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None) -> DeviceCall:
+    """encode_device(...) bound once; call the result to encode."""
+    ctx = ctx or default_context()
+    u = ctypes.c_uint64
+    args = (_vp(ctx.handle.value), _int(rate_), u(original_count), u(recovery_count), u(shard_bytes),
+            _vp(_ptr(d_original)), u(_row_stride(d_original)), _vp(_ptr(d_recovery)), u(_row_stride(d_recovery)),
+            _vp(_stream(stream)))
+    return DeviceCall(_lib.rs_encode_device_strided, args, (d_original, d_recovery, ctx))
+
+
+def decode_device_call(original_count: int, recovery_count: int, shard_bytes: int, d_original, original_present,
+                       d_recovery, recovery_present, d_restored, stream=None, rate_: int = RATE_DEFAULT,
+                       ctx: Optional[Context] = None) -> DeviceCall:
+    """decode_device(...) bound once; call the result to decode."""
+    ctx = ctx or default_context()
+    op = present_mask(original_present)
+    rp = present_mask(recovery_present)
+    u = ctypes.c_uint64
+    args = (_vp(ctx.handle.value), _int(rate_), u(original_count), u(recovery_count), u(shard_bytes),
+            _vp(_ptr(d_original)), u(_row_stride(d_original)), op, _vp(_ptr(d_recovery)),
+            u(_row_stride(d_recovery)), rp, _vp(_ptr(d_restored)), u(_row_stride(d_restored)), _vp(_stream(stream)))
+    return DeviceCall(_lib.rs_decode_device_strided, args, (d_original, d_recovery, d_restored, op, rp, ctx))
+
+
 _sig("rs_host_alloc", ctypes.c_void_p, _u64)
 _sig("rs_host_free", None, ctypes.c_void_p)
 _sig("rs_encode_host", _int, _vp, _int, _u64, _u64, _u64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,

@@ -703,3 +703,30 @@ def test_decode_loss_patterns_pruned_reveal(torch, rs, kind, rate, N, M, S, mono
         rs.check_device()
     finally:
         rs.mono_enable(1)
+
+
+def test_bound_device_calls_match_oracle(torch, rs):
+    """encode_device_call / decode_device_call (the bench's timed calls) = the oracle."""
+    N, M, S = 1024, 1024, 1024
+    orig = O.generate_original(N, S, 3)
+    want = O.encode("default", orig, M)
+    d_orig = _dev(torch, orig)
+    d_rec = torch.zeros((M, S), dtype=torch.uint8, device="cuda")
+    enc = rs.encode_device_call(N, M, S, d_orig, d_rec)
+    for _ in range(3):
+        enc()
+    torch.cuda.synchronize()
+    assert np.array_equal(d_rec.cpu().numpy(), want)
+    L = 11
+    op = np.ones(N, np.uint8)
+    op[N - L:] = 0
+    rp = np.zeros(M, np.uint8)
+    rp[:L] = 1
+    d_out = torch.full((N, S), 0x33, dtype=torch.uint8, device="cuda")
+    dec = rs.decode_device_call(N, M, S, d_orig, op, d_rec, rp, d_out)
+    dec()
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy()
+    assert np.array_equal(got[N - L:], orig[N - L:]) and np.all(got[:N - L] == 0x33)
+    with pytest.raises(rs.Error):
+        rs.encode_device_call(3, 70000, 64, d_orig, d_rec)()
