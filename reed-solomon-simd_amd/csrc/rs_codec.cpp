@@ -475,22 +475,22 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
 // A pruned FFT: the reference transforms every row (rate_high.rs:241-246) and
 // reads back only the erased ones, so the restored rows are the same bytes.
 constexpr size_t kFftRuns = 4;
-void fft_pass_pruned(rs::PassArgs P, const Levels &lv, uint32_t k, uint32_t nd, const std::vector<uint8_t> &st,
-                     const rs::RowMap &out, hipStream_t s) {
-    const uint32_t a = lv.lo[k], sb_log = a + lv.K[k], nsb = nd >> sb_log;
+
+// Launch a pass at level k over the sets of the superblocks (2^(lo_k + K_k)
+// rows) whose `weight` is nonzero, as at most kFftRuns runs of consecutive sets.
+void launch_runs(rs::PassArgs P, const Levels &lv, uint32_t k, int flags, const std::vector<uint64_t> &weight,
+                 hipStream_t s, bool wr_weight) {
+    const uint32_t a = lv.lo[k];
     std::vector<std::pair<uint32_t, uint32_t>> runs;  // [begin, end) superblocks
-    std::vector<uint64_t> erased;                      // erased rows in range per run
-    for (uint32_t sb = 0; sb < nsb; ++sb) {
-        const uint32_t r0 = std::max(sb << sb_log, out.row_begin), r1 = std::min((sb + 1) << sb_log, out.row_end);
-        uint64_t e = 0;
-        for (uint32_t r = r0; r < r1; ++r) e += st[r] == 1;
-        if (!e) continue;
+    std::vector<uint64_t> w;
+    for (uint32_t sb = 0; sb < weight.size(); ++sb) {
+        if (!weight[sb]) continue;
         if (!runs.empty() && runs.back().second == sb) {
             runs.back().second = sb + 1;
-            erased.back() += e;
+            w.back() += weight[sb];
         } else {
             runs.push_back({sb, sb + 1});
-            erased.push_back(e);
+            w.push_back(weight[sb]);
         }
     }
     while (runs.size() > kFftRuns) {
@@ -498,14 +498,29 @@ void fft_pass_pruned(rs::PassArgs P, const Levels &lv, uint32_t k, uint32_t nd, 
         for (size_t i = 1; i + 1 < runs.size(); ++i)
             if (runs[i + 1].first - runs[i].second < runs[j + 1].first - runs[j].second) j = i;
         runs[j].second = runs[j + 1].second;
-        erased[j] += erased[j + 1];
+        w[j] += w[j + 1];
         runs.erase(runs.begin() + j + 1);
-        erased.erase(erased.begin() + j + 1);
+        w.erase(w.begin() + j + 1);
     }
     for (size_t i = 0; i < runs.size(); ++i) {
         P.set_base = runs[i].first << a;
-        launch(int(lv.K[k]), rs::kFft, P, (runs[i].second - runs[i].first) << a, a, s, 0, P.reveal ? erased[i] : 0);
+        launch(int(lv.K[k]), flags, P, (runs[i].second - runs[i].first) << a, a, s, wr_weight ? 0 : w[i],
+               wr_weight ? w[i] : 0);
     }
+}
+
+// Rows r of [r_begin, r_end) with st[r] == want, counted per 2^sb_log-row superblock.
+std::vector<uint64_t> count_per_block(const std::vector<uint8_t> &st, uint32_t nd, uint32_t sb_log, uint32_t r_begin,
+                                      uint32_t r_end, uint8_t want) {
+    std::vector<uint64_t> c(nd >> sb_log, 0);
+    for (uint32_t r = r_begin; r < std::min(r_end, nd); ++r) c[r >> sb_log] += st[r] == want;
+    return c;
+}
+
+void fft_pass_pruned(rs::PassArgs P, const Levels &lv, uint32_t k, uint32_t nd, const std::vector<uint8_t> &st,
+                     const rs::RowMap &out, hipStream_t s) {
+    launch_runs(P, lv, k, rs::kFft, count_per_block(st, nd, lv.lo[k] + lv.K[k], out.row_begin, out.row_end, 1), s,
+                true);
 }
 
 // Decode (rate_high.rs:172-254 / rate_low.rs:172-254).  Only missing original
@@ -622,6 +637,21 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
     for (uint32_t k = 0; k + 1 < lv.m; ++k) X[k] = static_cast<uint8_t *>(ws.buf[k].get(size_t(nd) * g.stride));
     uint8_t *U = static_cast<uint8_t *>(ws.buf[3].get(size_t(nd) * g.stride));
     A.work_stride = g.stride;
+    // 2 levels: level-0 blocks (2^K0 rows) without a received row have a zero
+    // IFFT (not computed; read as zero), and the top pass stores U only for
+    // the blocks the pruned reveal pass reads
+    const uint32_t K0 = lv.K[0];
+    const bool masks = lv.m == 2 && (nd >> K0) <= 256;
+    std::vector<uint64_t> recv_blk, keep_blk;
+    if (masks) {
+        recv_blk = count_per_block(st, nd, K0, 0, nd, 2);
+        keep_blk = count_per_block(st, nd, K0, out_map.row_begin, out_map.row_end, 1);
+        for (uint32_t b = 0; b < recv_blk.size(); ++b) {
+            if (!recv_blk[b]) A.zero_in[b >> 6] |= 1ull << (b & 63);
+            if (!keep_blk[b]) A.keep_out[b >> 6] &= ~(1ull << (b & 63));
+        }
+        A.blk_shift = K0;
+    }
     for (uint32_t k = 0; k + 1 < lv.m; ++k) {  // scale received rows (level 0), IFFT low levels
         rs::PassArgs P = A;
         if (k == 0) {
@@ -633,13 +663,18 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
             P.work_in = X[k - 1];
         }
         P.work_out = X[k];
-        run_level(P, lv, k, rs::kIfft, nd, s, k == 0 ? received : 0, 0);
+        if (masks)
+            launch_runs(P, lv, 0, rs::kIfft, recv_blk, s, false);
+        else
+            run_level(P, lv, k, rs::kIfft, nd, s, k == 0 ? received : 0, 0);
     }
     rs::PassArgs T = A;  // top: IFFT, its derivative terms, FFT -> U
     T.work_in = X[lv.m - 2];
     T.fd_mode = 1;
     T.work_out = U;
+    T.blk_masks = masks ? 1 : 0;
     run_level(T, lv, lv.m - 1, rs::kIfft | rs::kFft, nd, s);
+    A.blk_masks = masks ? 1 : 0;  // the reveal pass reads X[0]: zero blocks load as zero
     for (int k = int(lv.m) - 2; k >= 0; --k) {  // V_k, last one revealed
         rs::PassArgs P = A;
         P.work_in = X[k];

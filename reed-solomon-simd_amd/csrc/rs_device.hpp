@@ -53,6 +53,13 @@ struct PassArgs {
 
     const uint32_t *tw = nullptr;       // perm tables indexed by skew index (zero table = no multiply)
     const uint32_t *lut = nullptr;      // perm tables indexed by log factor
+
+    // ---- 2-level decodes (blk_masks = 1): per block b = row >> blk_shift (b < 256),
+    // zero_in bit b: the block's work_in rows are zero (never computed; load as zero);
+    // keep_out bit b: the block's work_out rows are read later (others are not stored)
+    uint32_t blk_masks = 0, blk_shift = 0;
+    uint64_t zero_in[4] = {0, 0, 0, 0};
+    uint64_t keep_out[4] = {~0ull, ~0ull, ~0ull, ~0ull};
 };
 
 enum PassFlags {

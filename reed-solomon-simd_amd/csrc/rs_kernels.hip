@@ -225,6 +225,12 @@ __device__ __forceinline__ void stage_twiddles(const PassArgs &A, const Ctx &c, 
     st.store();
 }
 
+// Bit b (< 256) of a 4-word block mask: uniform words, per-lane selects.
+__device__ __forceinline__ bool blk_bit(const uint64_t (&m)[4], uint32_t b) {
+    const uint64_t w = b < 128 ? (b < 64 ? m[0] : m[1]) : (b < 192 ? m[2] : m[3]);
+    return (w >> (b & 63u)) & 1u;
+}
+
 // Load the lane's rows (phase PH) of `chunk`.  SCALE: rows erased in the
 // decode's erasure vector load as zero (checked in global rowinfo, so the
 // load need not wait for staging).
@@ -241,7 +247,8 @@ __device__ __forceinline__ void load_rows(const PassArgs &A, const Ctx &c, uint3
         static_for<0, P::R>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             uint32_t l = 0, h = 0;
-            if (c.pk_ok) {
+            const uint32_t r = r0 + (uint32_t(i) << (P::start(PH) + c.a));
+            if (c.pk_ok && !(A.blk_masks && blk_bit(A.zero_in, r >> A.blk_shift))) {
                 const uint8_t *p = p0 + step * uint64_t(i);
                 l = ld32(p);
                 h = ld32(p + 32);
@@ -321,7 +328,8 @@ __device__ __forceinline__ void store_rows(const PassArgs &A, const Ctx &c, uint
         const uint64_t step = A.work_stride << (P::start(PH) + c.a);
         static_for<0, P::R>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
-            if (c.pk_ok) {
+            const uint32_t r = r0 + (uint32_t(i) << (P::start(PH) + c.a));
+            if (c.pk_ok && !(A.blk_masks && !blk_bit(A.keep_out, r >> A.blk_shift))) {
                 uint8_t *p = p0 + step * uint64_t(i);
                 st32(p, lo[i]);
                 st32(p + 32, hi[i]);
