@@ -475,22 +475,40 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
 // A pruned FFT: the reference transforms every row (rate_high.rs:241-246) and
 // reads back only the erased ones, so the restored rows are the same bytes.
 constexpr size_t kFftRuns = 4;
+constexpr uint64_t kBridgeBytes = uint64_t(128) << 20;
+constexpr uint64_t kKeepOutRowBytes = 8192;
 
 // Launch a pass at level k over the sets of the superblocks (2^(lo_k + K_k)
 // rows) whose `weight` is nonzero, as at most kFftRuns runs of consecutive sets.
+// `rows` (optional): rows read (IFFT) or written (reveal) per superblock, for
+// the profiler's byte counts; else `weight` is that count.
 void launch_runs(rs::PassArgs P, const Levels &lv, uint32_t k, int flags, const std::vector<uint64_t> &weight,
-                 hipStream_t s, bool wr_weight) {
+                 hipStream_t s, bool wr_weight, const std::vector<uint64_t> *rows = nullptr) {
     const uint32_t a = lv.lo[k];
     std::vector<std::pair<uint32_t, uint32_t>> runs;  // [begin, end) superblocks
     std::vector<uint64_t> w;
     for (uint32_t sb = 0; sb < weight.size(); ++sb) {
         if (!weight[sb]) continue;
+        const uint64_t n = rows ? (*rows)[sb] : weight[sb];
         if (!runs.empty() && runs.back().second == sb) {
             runs.back().second = sb + 1;
-            w.back() += weight[sb];
+            w.back() += n;
         } else {
             runs.push_back({sb, sb + 1});
-            w.push_back(weight[sb]);
+            w.push_back(n);
+        }
+    }
+    // a gap of fewer than kBridgeBytes of rows costs less to transform than a
+    // launch of its own (measured: 32768:32768 x 1 KiB, 1 % loss, profiles/r01o)
+    const uint64_t set_bytes = (uint64_t(P.packs) * 8) << lv.K[k];
+    for (size_t i = 0; i + 1 < runs.size();) {
+        if (uint64_t(runs[i + 1].first - runs[i].second) * set_bytes << a < kBridgeBytes) {
+            runs[i].second = runs[i + 1].second;
+            w[i] += w[i + 1];
+            runs.erase(runs.begin() + i + 1);
+            w.erase(w.begin() + i + 1);
+        } else {
+            ++i;
         }
     }
     while (runs.size() > kFftRuns) {
@@ -509,11 +527,17 @@ void launch_runs(rs::PassArgs P, const Levels &lv, uint32_t k, int flags, const 
     }
 }
 
-// Rows r of [r_begin, r_end) with st[r] == want, counted per 2^sb_log-row superblock.
+// Rows r of [r_begin, r_end) with st[r] == want, counted per 2^sb_log-row
+// superblock (std::count over each block's bytes: vectorised; this runs on the
+// host for every decode, ahead of launches that take ~100 us for 2^16 rows).
 std::vector<uint64_t> count_per_block(const std::vector<uint8_t> &st, uint32_t nd, uint32_t sb_log, uint32_t r_begin,
                                       uint32_t r_end, uint8_t want) {
     std::vector<uint64_t> c(nd >> sb_log, 0);
-    for (uint32_t r = r_begin; r < std::min(r_end, nd); ++r) c[r >> sb_log] += st[r] == want;
+    r_end = std::min(r_end, nd);
+    for (uint32_t sb = 0; sb < c.size(); ++sb) {
+        const uint32_t r0 = std::max(sb << sb_log, r_begin), r1 = std::min((sb + 1) << sb_log, r_end);
+        if (r0 < r1) c[sb] = uint64_t(std::count(st.data() + r0, st.data() + r1, want));
+    }
     return c;
 }
 
@@ -637,21 +661,51 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
     for (uint32_t k = 0; k + 1 < lv.m; ++k) X[k] = static_cast<uint8_t *>(ws.buf[k].get(size_t(nd) * g.stride));
     uint8_t *U = static_cast<uint8_t *>(ws.buf[3].get(size_t(nd) * g.stride));
     A.work_stride = g.stride;
-    // 2 levels: level-0 blocks (2^K0 rows) without a received row have a zero
-    // IFFT (not computed; read as zero), and the top pass stores U only for
-    // the blocks the pruned reveal pass reads
-    const uint32_t K0 = lv.K[0];
-    const bool masks = lv.m == 2 && (nd >> K0) <= 256;
-    std::vector<uint64_t> recv_blk, keep_blk;
+    // Blocks of 2^G rows, G = the top level's lowest bit (2^K_top <= 256 blocks):
+    // a block with no received row has a zero IFFT below the top level (not
+    // computed; read as zero), and the passes from the top down store U only
+    // for the blocks the pruned FFT passes read
+    const uint32_t G = lv.lo[lv.m - 1];
+    // A/B measurement switch: 1 = no block masks, 2 = no IFFT-pass pruning (store masks only)
+    static const int prune_mode = getenv("RS_MI355X_DECODE_PRUNE") ? atoi(getenv("RS_MI355X_DECODE_PRUNE")) : 0;
+    const bool masks = prune_mode != 1 && (nd >> G) <= 256;
+    const bool prune_ifft = masks && prune_mode != 2;
+    std::vector<uint64_t> recv_blk;
+    bool skips = false;  // some block's IFFT is skipped
     if (masks) {
-        recv_blk = count_per_block(st, nd, K0, 0, nd, 2);
-        keep_blk = count_per_block(st, nd, K0, out_map.row_begin, out_map.row_end, 1);
-        for (uint32_t b = 0; b < recv_blk.size(); ++b) {
-            if (!recv_blk[b]) A.zero_in[b >> 6] |= 1ull << (b & 63);
-            if (!keep_blk[b]) A.keep_out[b >> 6] &= ~(1ull << (b & 63));
+        recv_blk = count_per_block(st, nd, G, 0, nd, 2);
+        if (prune_ifft) {  // the blocks the IFFT passes launch: runs as launch_runs bridges them
+            const uint64_t blk_bytes = (uint64_t(g.packs) * 8) << G;
+            std::vector<std::pair<uint32_t, uint32_t>> runs;
+            for (uint32_t b = 0; b < recv_blk.size(); ++b) {
+                if (!recv_blk[b]) continue;
+                if (!runs.empty() && (b - runs.back().second) * blk_bytes < kBridgeBytes) runs.back().second = b + 1;
+                else runs.push_back({b, b + 1});
+            }
+            std::vector<uint64_t> live(recv_blk.size(), 0);
+            for (size_t i = 0; i < runs.size(); ++i) {
+                // beyond kFftRuns runs the launcher bridges the smallest gaps: keep those blocks live
+                const uint32_t end = i + 1 < runs.size() && runs.size() > kFftRuns ? runs[i + 1].first : runs[i].second;
+                for (uint32_t b = runs[i].first; b < end; ++b) live[b] = 1;
+            }
+            for (uint32_t b = 0; b < recv_blk.size(); ++b) {
+                if (!live[b]) {
+                    A.zero_in[b >> 6] |= 1ull << (b & 63);
+                    skips = true;
+                }
+                recv_blk[b] = live[b];
+            }
         }
-        A.blk_shift = K0;
+        // U stores are skipped per row only where rows are long enough for the
+        // saved write to outweigh the per-row test (measured, profiles/r01o)
+        if (uint64_t(g.packs) * 8 >= kKeepOutRowBytes) {
+            const std::vector<uint64_t> keep_blk = count_per_block(st, nd, G, out_map.row_begin, out_map.row_end, 1);
+            for (uint32_t b = 0; b < keep_blk.size(); ++b)
+                if (!keep_blk[b]) A.keep_out[b >> 6] &= ~(1ull << (b & 63));
+        }
+        A.blk_shift = G;
     }
+    const bool top_masks = masks && (skips || uint64_t(g.packs) * 8 >= kKeepOutRowBytes);
     for (uint32_t k = 0; k + 1 < lv.m; ++k) {  // scale received rows (level 0), IFFT low levels
         rs::PassArgs P = A;
         if (k == 0) {
@@ -663,18 +717,24 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
             P.work_in = X[k - 1];
         }
         P.work_out = X[k];
-        if (masks)
-            launch_runs(P, lv, 0, rs::kIfft, recv_blk, s, false);
-        else
+        if (prune_ifft) {  // level-k superblocks inside blocks with received rows
+            const uint32_t sb_log = lv.lo[k] + lv.K[k];
+            std::vector<uint64_t> w(nd >> sb_log), rd(nd >> sb_log, 0);
+            for (uint32_t sb = 0; sb < w.size(); ++sb) w[sb] = recv_blk[(sb << sb_log) >> G];
+            if (k == 0 && t_prof_ctx) rd = count_per_block(st, nd, sb_log, 0, nd, 2);  // profiler bytes only
+            launch_runs(P, lv, k, rs::kIfft, w, s, false, &rd);
+        } else {
             run_level(P, lv, k, rs::kIfft, nd, s, k == 0 ? received : 0, 0);
+        }
     }
     rs::PassArgs T = A;  // top: IFFT, its derivative terms, FFT -> U
     T.work_in = X[lv.m - 2];
     T.fd_mode = 1;
     T.work_out = U;
-    T.blk_masks = masks ? 1 : 0;
+    T.blk_masks = top_masks ? 1 : 0;
     run_level(T, lv, lv.m - 1, rs::kIfft | rs::kFft, nd, s);
-    A.blk_masks = masks ? 1 : 0;  // the reveal pass reads X[0]: zero blocks load as zero
+    A.blk_masks = skips ? 1 : 0;  // the passes below the top read X[k]: zero blocks load as zero
+    A.blk_uniform = 1;
     for (int k = int(lv.m) - 2; k >= 0; --k) {  // V_k, last one revealed
         rs::PassArgs P = A;
         P.work_in = X[k];

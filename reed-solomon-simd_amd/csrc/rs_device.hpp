@@ -57,7 +57,9 @@ struct PassArgs {
     // ---- 2-level decodes (blk_masks = 1): per block b = row >> blk_shift (b < 256),
     // zero_in bit b: the block's work_in rows are zero (never computed; load as zero);
     // keep_out bit b: the block's work_out rows are read later (others are not stored)
-    uint32_t blk_masks = 0, blk_shift = 0;
+    // blk_uniform = 1: every row set of the launch lies inside one block (the
+    // passes below the top level): one scalar test per workgroup, no store mask
+    uint32_t blk_masks = 0, blk_shift = 0, blk_uniform = 0;
     uint64_t zero_in[4] = {0, 0, 0, 0};
     uint64_t keep_out[4] = {~0ull, ~0ull, ~0ull, ~0ull};
 };

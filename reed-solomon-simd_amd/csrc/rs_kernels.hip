@@ -244,11 +244,14 @@ __device__ __forceinline__ void load_rows(const PassArgs &A, const Ctx &c, uint3
         const uint32_t r0 = c.grow(P::template lrow<PH>(c.g, 0), K) + chunk * A.n;
         const uint8_t *p0 = A.work_in + uint64_t(r0) * A.work_stride + c.pk_off;
         const uint64_t step = A.work_stride << (P::start(PH) + c.a);
+        const bool per_row = A.blk_masks && !A.blk_uniform;
+        const bool zero_set = A.blk_masks && A.blk_uniform &&
+                              blk_bit(A.zero_in, __builtin_amdgcn_readfirstlane(r0 >> A.blk_shift));
         static_for<0, P::R>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             uint32_t l = 0, h = 0;
             const uint32_t r = r0 + (uint32_t(i) << (P::start(PH) + c.a));
-            if (c.pk_ok && !(A.blk_masks && blk_bit(A.zero_in, r >> A.blk_shift))) {
+            if (c.pk_ok && !zero_set && !(per_row && blk_bit(A.zero_in, r >> A.blk_shift))) {
                 const uint8_t *p = p0 + step * uint64_t(i);
                 l = ld32(p);
                 h = ld32(p + 32);
@@ -329,7 +332,7 @@ __device__ __forceinline__ void store_rows(const PassArgs &A, const Ctx &c, uint
         static_for<0, P::R>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             const uint32_t r = r0 + (uint32_t(i) << (P::start(PH) + c.a));
-            if (c.pk_ok && !(A.blk_masks && !blk_bit(A.keep_out, r >> A.blk_shift))) {
+            if (c.pk_ok && !(A.blk_masks && !A.blk_uniform && !blk_bit(A.keep_out, r >> A.blk_shift))) {
                 uint8_t *p = p0 + step * uint64_t(i);
                 st32(p, lo[i]);
                 st32(p + 32, hi[i]);
