@@ -135,23 +135,32 @@ __global__ void __launch_bounds__(512) k_walsh_part(const EvalArgs A, uint32_t a
         sv[j] = x;
     }
     __syncthreads();
-    for (uint32_t h = 0; h < K; ++h) {
-        for (uint32_t k = threadIdx.x; k < m / 2; k += blockDim.x) {
-            const uint32_t i = ((k >> h) << (h + 1)) | (k & ((1u << h) - 1u));
-            const uint32_t p = sv[i], q = sv[i + (1u << h)];
-            sv[i] = add_mod(p, q);
-            sv[i + (1u << h)] = sub_mod(p, q);
+    const auto walsh = [&]() {
+        for (uint32_t h = 0; h < K; ++h) {
+            for (uint32_t k = threadIdx.x; k < m / 2; k += blockDim.x) {
+                const uint32_t i = ((k >> h) << (h + 1)) | (k & ((1u << h) - 1u));
+                const uint32_t p = sv[i], q = sv[i + (1u << h)];
+                sv[i] = add_mod(p, q);
+                sv[i + (1u << h)] = sub_mod(p, q);
+            }
+            __syncthreads();
+        }
+    };
+    walsh();
+    if constexpr (STEP == 1) {  // x lw_fold between the two transforms' high-bit layers
+        for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
+            const uint32_t i = lo + (j << a) + (hi << (a + K));
+            const uint32_t p = sv[j] * A.lw_fold[i];
+            uint32_t x = add_mod(p & 0xFFFFu, p >> 16);
+            if (A.low_rate && i == 0) x = add_mod(x, A.lw0);
+            sv[j] = x;
         }
         __syncthreads();
+        walsh();
     }
     for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
         const uint32_t i = lo + (j << a) + (hi << (a + K));
         uint32_t x = sv[j];
-        if constexpr (STEP == 1) {
-            const uint32_t p = x * A.lw_fold[i];
-            x = add_mod(p & 0xFFFFu, p >> 16);
-            if (A.low_rate && i == 0) x = add_mod(x, A.lw0);
-        }
         if constexpr (STEP == 3) x |= state_bit(A, i, 1) ? 0u : 0x10000u;
         A.rowinfo[i] = x;
     }
@@ -167,10 +176,12 @@ hipError_t launch_eval_poly(const EvalArgs &A, hipStream_t s) {
             const uint32_t m = 1u << K;
             kern<<<n >> K, m / 2 < 64 ? 64 : (m / 2 > 512 ? 512 : m / 2), size_t(4) * m, s>>>(A, a, K);
         };
+        // Walsh-Hadamard layers on different bits commute: low bits of the
+        // first transform; high bits of both around the multiply (one launch);
+        // low bits of the second transform + output
         go(k_walsh_part<0>, 0, K1);
         go(k_walsh_part<1>, K1, K2);
-        go(k_walsh_part<2>, 0, K1);
-        go(k_walsh_part<3>, K1, K2);
+        go(k_walsh_part<3>, 0, K1);
         return hipGetLastError();
     }
     const size_t lds = size_t(2) * (n < 2 ? 2 : n) + size_t(8) * ((n + 31) / 32);
