@@ -172,7 +172,10 @@ def main():
                 "traffic": traffic["hbm_bytes"] if traffic else None,
                 "traffic_source": traffic["source"] if traffic else None,
                 "algorithmic_bytes": alg_step,
-                "avg_us": round(dom_avg_s * 1e6, 3), "kernels": kernels}
+                "avg_us": round(dom_avg_s * 1e6, 3), "kernels": kernels,
+                "note": "avg_us: the timed batch's launch-stream event time / steps when one launch is the "
+                        "whole step (rocprofv3 kernel-trace average agrees, profiles/); kernels[].avg_us "
+                        "brackets every launch with its own events, which adds their overhead"}
 
     # ---- decode at 1 % and 100 % loss (benchmarks.rs:113-138) --------------
     decode = {}
