@@ -217,8 +217,12 @@ constexpr uint32_t kMaxK = 8;  // pass kernels exist for K <= 8
 // (32768:32768 x 64 KiB encode 820 -> 884 GiB/s; at 1 KiB shards 656 -> 505).
 constexpr uint64_t kMaxBatchStripes = 65535;  // stripes per column-kernel launch (grid.y)
 uint32_t g_max_k = 0;  // RS_MI355X_MAX_K (4..8) overrides the choice below
-uint32_t max_k_enc(uint32_t packs) { return g_max_k ? g_max_k : packs >= 2048 ? 8 : 7; }
-uint32_t max_k_dec() { return g_max_k ? g_max_k : 7; }
+// Measured with the pruned decode passes (profiles/r01p/ab_maxk_*, tools/ab_maxk.sh):
+// encodes run fastest with 8-bit levels (32768:32768 x 1 KiB 671 -> 711 GiB/s vs 7),
+// decodes with 6-bit levels (8192:8192 x 64 KiB 1 % / 100 %: 637 / 531 -> 840 / 641 GiB/s:
+// more levels below the top, so more of the FFT is pruned and more IFFT blocks skipped)
+uint32_t max_k_enc(uint32_t) { return g_max_k ? g_max_k : 8; }
+uint32_t max_k_dec() { return g_max_k ? g_max_k : 6; }
 struct Levels {
     uint32_t m = 0;
     uint32_t lo[4] = {0, 0, 0, 0}, K[4] = {0, 0, 0, 0};
