@@ -8,20 +8,33 @@ encode of one 1024:1024 x 1 KiB stripe whose shards already sit in HBM
 (loss pattern of the reference's benches/benchmarks.rs:113-138) is timed the
 same way and reported beside the headline value.
 
-N > 1 (torchrun, one process per GPU): every rank encodes its own stripes
-(independent objects, no data-path collective) -> "scaling": "weak"; value =
-bytes of all ranks / max-over-ranks time.
+--gpus N > 1: the parent process (which never touches the GPU) starts N ranks
+with torch.distributed.run, one process per GPU (RCCL = the "nccl" backend).
+The default workload at N > 1 is north_star's multi-GPU configuration,
+configs[4]: ONE 32768:32768 x 64 KiB stripe column-partitioned over the ranks
+(rank r encodes byte columns [r*S/N, (r+1)*S/N) of every shard) followed by an
+RCCL all-gather of the recovery slices over xGMI and a re-interleave; total
+work is fixed -> "scaling": "strong".  --config selects any other workload
+(the 1-GPU configs then run as independent stripes per rank: weak scaling).
 
-roofline: per-kernel HIP-event timing of the launches of the timed workload
-(rs_profile_enable), dominant kernel = largest total time; achieved = its
-algorithmic bytes per launch / its average duration; peak = 8 TB/s HBM3E.
-cpu_baseline: the reference's AVX2 algorithm restated in C (oracle/avx2_port.c),
-single thread, on a bounded sample, rank 0 at N = 1 only.
+Timing: W untimed warmup steps, then exactly K steps bracketed by a barrier +
+torch.cuda.synchronize() on both sides, max over ranks.  Nothing else runs in
+the timed region (HIP events of the kernels are taken in a separate pass).
+
+roofline: per-launch HIP events on the launch stream (rs_profile_enable) over
+the same workload; dominant kernel = largest total time; achieved = the
+SURVEY.md 8(d) algorithmic bytes / duration; peak = 8 TB/s HBM3E; traffic =
+HBM bytes per launch of that kernel from the committed rocprofv3 PMC passes
+(profiles/<tag>/traffic.json); valu_frac = VALU wave-instructions per launch
+(SQ_INSTS_VALU, same summary) x 2 cycles / (duration x 1024 SIMDs x 2.4 GHz).
+cpu_baseline: the reference's AVX2 algorithm restated in C (oracle/avx2_port.c)
+on a bounded sample of the same workload, rank 0.
 """
 import argparse
 import json
 import os
-import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,6 +44,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 METRIC = "GiB/s (original+recovery) encode & decode, device-resident, 1024:1024×1024B"
 HBM_PEAK_GBS = 8000.0
+SIMDS, CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 2  # MI355X: 256 CUs x 4 SIMDs; a wave64 VALU op issues over 2 cycles
 
 CONFIGS = {
     # name: (original_count, recovery_count, shard_bytes)
@@ -39,7 +53,44 @@ CONFIGS = {
     "8192x8192x64k": (8192, 8192, 65536),      # configs[3] (decode)
     "32768x32768x64k": (32768, 32768, 65536),  # configs[4] (column-partitioned over the ranks)
 }
+HEADLINE = "1024x1024x1k"
 SHARDED = "32768x32768x64k"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                   help=f"default: {HEADLINE} on 1 GPU, {SHARDED} (column-partitioned) on N > 1")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-copy", action="store_true", help="skip the 1 GiB device-copy context measurement")
+    p.add_argument("--no-decode", action="store_true")
+    p.add_argument("--no-host", action="store_true", help="skip the host-memory end-to-end measurement")
+    p.add_argument("--profile-steps", type=int, default=50)
+    p.add_argument("--batch", type=int, default=64, help="stripes per call of the batched measurement (1 = skip)")
+    p.add_argument("--plumbing", action="store_true",
+                   help="CPU/gloo check of the rank launcher and timing reduction (no GPU, no kernels)")
+    return p.parse_args()
+
+
+# ---------------------------------------------------------------------------
+# rank launcher: the parent never initialises the GPU
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def reduce_max(x, world, device):
@@ -54,90 +105,138 @@ def reduce_max(x, world, device):
     return float(t.item())
 
 
-def parse():
-    p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--config", default="1024x1024x1k", choices=sorted(CONFIGS))
-    p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--no-copy", action="store_true", help="skip the 1 GiB device-copy context measurement")
-    p.add_argument("--no-decode", action="store_true")
-    p.add_argument("--no-host", action="store_true", help="skip the host-memory end-to-end measurement")
-    p.add_argument("--profile-steps", type=int, default=50)
-    p.add_argument("--batch", type=int, default=64, help="stripes per call of the batched measurement (1 = skip)")
-    return p.parse_args()
+def plumbing(args, world, rank):
+    """--plumbing: the multi-rank skeleton of the bench on gloo (CPU tests)."""
+    import torch
+    import torch.distributed as dist
+
+    for _ in range(args.warmup):
+        pass
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001)
+    wall = reduce_max(time.perf_counter() - t0, world, "cpu")
+    ranks = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(ranks, torch.tensor([rank], dtype=torch.int64))
+    if rank == 0:
+        print(json.dumps({"metric": "plumbing", "value": round(args.steps / wall, 3), "unit": "steps/s",
+                          "n_gpus": world if world > 1 else 1, "steps": args.steps, "warmup": args.warmup,
+                          "ranks_seen": [int(r.item()) for r in ranks] if world > 1 else [0]}))
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.plumbing:
+        if world > 1:
+            dist.init_process_group("gloo")
+        plumbing(args, world, rank)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()
     torch.cuda.set_device(local)
     import reed_solomon_simd as rs
 
     ctx = rs.Context(local)
-    N, M, S = CONFIGS[args.config]
+    config = args.config or (SHARDED if world > 1 else HEADLINE)
     dev = torch.device("cuda", local)
-    if args.config == SHARDED:
+    if config == SHARDED:
         sharded_bench(args, rs, ctx, world, rank, dev)
-        if world > 1:
-            dist.destroy_process_group()
-        return
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)
-    d_orig = torch.randint(0, 256, (N, S), dtype=torch.uint8, device=dev, generator=g)
-    d_rec = torch.empty((M, S), dtype=torch.uint8, device=dev)
-    d_out = torch.empty((N, S), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.Stream(device=dev)
+    else:
+        stripe_bench(args, rs, ctx, config, world, rank, dev)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------
+# timing helpers
+
+def make_timer(world, dev):
+    import torch
+    import torch.distributed as dist
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    def max_over_ranks(x):
-        return reduce_max(x, world, dev)
-
     def timed(fn, steps, warmup):
-        with torch.cuda.stream(stream):
-            for _ in range(warmup):
-                fn()
+        """Wall time of exactly `steps` calls of fn, bracketed by barrier + synchronize; max over ranks."""
+        for _ in range(warmup):
+            fn()
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
-        with torch.cuda.stream(stream):
-            ev0.record(stream)
-            for _ in range(steps):
-                fn()
-            ev1.record(stream)
+        for _ in range(steps):
+            fn()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         barrier()
-        return max_over_ranks(wall), max_over_ranks(ev0.elapsed_time(ev1) / 1e3)
+        return reduce_max(wall, world, dev)
 
-    # one C-ABI call per step (rs_encode_device_strided), arguments bound once:
-    # the Python keyword wrapper would add ≈3 µs of host time to an 8 µs step
-    enc = rs.encode_device_call(N, M, S, d_orig, d_rec, stream=stream, ctx=ctx)
+    def gpu_time(fn, steps, stream):
+        """GPU time of `steps` calls from events on the launch stream (separate, untimed pass)."""
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        ev0.record(stream)
+        for _ in range(steps):
+            fn()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        return reduce_max(ev0.elapsed_time(ev1) / 1e3, world, dev)
 
-    # ---- headline: encode -------------------------------------------------
-    wall, gpu_t = timed(enc, args.steps, args.warmup)
-    step_bytes = (N + M) * S
-    value = step_bytes * args.steps * world / wall / 2**30
+    return timed, gpu_time
 
-    # ---- per-kernel timing of the same workload ----------------------------
+
+def load_pmc(kernel, config):
+    """Per-launch PMC figures of `kernel` in the bench of `config` from the newest committed
+    summary that has them (profiles/<tag>/traffic.json, written by tools/pmc_traffic.py from
+    rocprofv3 --pmc passes over this bench): HBM bytes (FETCH_SIZE x2 + WRITE_SIZE) and
+    SQ_INSTS_VALU."""
+    pdir = os.path.join(ROOT, "profiles")
+    out = {}
+    if not os.path.isdir(pdir):
+        return out
+    for tag in sorted(os.listdir(pdir), reverse=True):
+        f = os.path.join(pdir, tag, "traffic.json")
+        if not os.path.exists(f):
+            continue
+        with open(f) as fh:
+            d = json.load(fh)
+        k = d["configs"].get(config, {}).get(kernel) if "configs" in d else (
+            d["kernels"].get(kernel) if config == HEADLINE else None)
+        if not k:
+            continue
+        if "traffic" not in out and "hbm_bytes" in k:
+            out["traffic"] = (k["hbm_bytes"], f"profiles/{tag}/traffic.json")
+        if "valu" not in out and "valu_insts" in k:
+            out["valu"] = (k["valu_insts"], f"profiles/{tag}/traffic.json")
+        if len(out) == 2:
+            break
+    return out
+
+
+def roofline_of(rs, ctx, fn, profile_steps, alg_step_bytes, config, launch_scope_s=None):
+    """Per-kernel HIP-event timing of `profile_steps` calls of fn (rs_profile_enable) and the
+    roofline block of the dominant kernel."""
+    import torch
+
     rs.profile_enable(True, ctx=ctx)
-    with torch.cuda.stream(stream):
-        for _ in range(args.profile_steps):
-            enc()
+    for _ in range(profile_steps):
+        fn()
     torch.cuda.synchronize()
     recs = rs.profile_collect(ctx)
     rs.profile_enable(False, ctx=ctx)
@@ -147,35 +246,61 @@ def main():
         a[0] += ms
         a[1] += 1
         a[2] += by
-    kernels = {k: {"launches_per_step": v[1] / args.profile_steps, "avg_us": round(1e3 * v[0] / v[1], 3),
-                   "rows_bytes_per_launch": v[2] // v[1]} for k, v in agg.items()}
+    kernels = {k: {"launches_per_step": v[1] / profile_steps, "avg_us": round(1e3 * v[0] / v[1], 3),
+                   "alg_bytes_per_launch": v[2] // v[1]} for k, v in agg.items()}
     dom = max(agg, key=lambda k: agg[k][0])
-    dom_avg_s = agg[dom][0] / agg[dom][1] / 1e3
-    # Algorithmic bytes: an encode must read N*S original
-    # bytes and write M*S recovery bytes.  When one launch does the whole
-    # encode (the headline's column kernel) that is its per-launch figure;
-    # otherwise the step's algorithmic bytes are priced against the summed
-    # duration of all the step's launches.
-    alg_step = (N + M) * S
-    kernel_s_per_step = sum(v[0] for v in agg.values()) / 1e3 / args.profile_steps
-    if len(agg) == 1 and kernels[dom]["launches_per_step"] == 1:
-        # one launch per step: its duration is the step's GPU time measured
-        # around the whole timed batch on the launch stream (gpu_t); events
-        # bracketing every single launch add their own gaps (kernels[...].avg_us)
-        dom_avg_s = gpu_t / args.steps
-        scope, achieved = "launch", alg_step / dom_avg_s / 1e9
+    kernel_s_per_step = sum(v[0] for v in agg.values()) / 1e3 / profile_steps
+    if len(agg) == 1 and kernels[dom]["launches_per_step"] == 1 and launch_scope_s:
+        # one launch per step: its duration is the step's GPU time measured around a whole
+        # batch on the launch stream; events bracketing every single launch add their own gaps
+        dom_avg_s = launch_scope_s
+        scope, achieved = "launch", alg_step_bytes / dom_avg_s / 1e9
     else:
-        scope, achieved = "step (all launches)", alg_step / kernel_s_per_step / 1e9
-    traffic = load_traffic(dom)
-    roofline = {"bound": "hbm", "kernel": dom, "scope": scope, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": traffic["hbm_bytes"] if traffic else None,
-                "traffic_source": traffic["source"] if traffic else None,
-                "algorithmic_bytes": alg_step,
-                "avg_us": round(dom_avg_s * 1e6, 3), "kernels": kernels,
-                "note": "avg_us: the timed batch's launch-stream event time / steps when one launch is the "
-                        "whole step (rocprofv3 kernel-trace average agrees, profiles/); kernels[].avg_us "
-                        "brackets every launch with its own events, which adds their overhead"}
+        dom_avg_s = agg[dom][0] / agg[dom][1] / 1e3
+        scope, achieved = "step (all launches)", alg_step_bytes / kernel_s_per_step / 1e9
+    pmc = load_pmc(dom, config)
+    valu = None
+    if "valu" in pmc:
+        insts = pmc["valu"][0]
+        valu = {"valu_insts_per_launch": insts, "frac": round(insts * VALU_CYCLES / (dom_avg_s * CLOCK_HZ * SIMDS), 4),
+                "source": pmc["valu"][1],
+                "note": "SQ_INSTS_VALU x 2 cycles per wave-instruction / (launch duration x 1024 SIMDs x 2.4 GHz)"}
+    return {"bound": "hbm", "kernel": dom, "scope": scope, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": pmc["traffic"][0] if "traffic" in pmc else None,
+            "traffic_source": pmc["traffic"][1] if "traffic" in pmc else None,
+            "algorithmic_bytes": alg_step_bytes, "avg_us": round(dom_avg_s * 1e6, 3),
+            "valu_frac": valu["frac"] if valu else None, "valu": valu, "kernels": kernels,
+            "note": "scope 'launch': one launch is the whole step, avg_us = launch-stream event time of a whole "
+                    "batch / steps (rocprofv3 kernel-trace average agrees, profiles/); otherwise achieved = the "
+                    "step's algorithmic bytes / the summed durations of the step's launches"}
+
+
+# ---------------------------------------------------------------------------
+# one stripe per step (configs[1..3]); N > 1: independent stripes per rank
+
+def stripe_bench(args, rs, ctx, config, world, rank, dev):
+    import torch
+
+    N, M, S = CONFIGS[config]
+    timed, gpu_time = make_timer(world, dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    d_orig = torch.randint(0, 256, (N, S), dtype=torch.uint8, device=dev, generator=g)
+    d_rec = torch.empty((M, S), dtype=torch.uint8, device=dev)
+    d_out = torch.empty((N, S), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.Stream(device=dev)
+
+    # one C-ABI call per step (rs_encode_device_strided), arguments bound once:
+    # the Python keyword wrapper would add ≈3 µs of host time to an 8 µs step
+    enc = rs.encode_device_call(N, M, S, d_orig, d_rec, stream=stream, ctx=ctx)
+
+    # ---- headline: encode -------------------------------------------------
+    wall = timed(enc, args.steps, args.warmup)
+    gpu_t = gpu_time(enc, args.steps, stream)
+    step_bytes = (N + M) * S
+    value = step_bytes * args.steps * world / wall / 2**30
+    roofline = roofline_of(rs, ctx, enc, args.profile_steps, step_bytes, config, gpu_t / args.steps)
 
     # ---- decode at 1 % and 100 % loss (benchmarks.rs:113-138) --------------
     decode = {}
@@ -184,13 +309,17 @@ def main():
             L = -(-min(N, M) * pct // 100)
             op = rs.present_mask([1] * (N - L) + [0] * L)
             rp = rs.present_mask([1] * L + [0] * (M - L))
-
             dec = rs.decode_device_call(N, M, S, d_orig, op, d_rec, rp, d_out, stream=stream, ctx=ctx)
-
-            w, gt = timed(dec, args.steps, args.warmup)
+            w = timed(dec, args.steps, args.warmup)
+            gt = gpu_time(dec, args.steps, stream)
             decode[f"{pct}pct"] = round(step_bytes * args.steps * world / w / 2**30, 3)
             decode[f"{pct}pct_us_per_step"] = {"wall": round(w / args.steps * 1e6, 2),
                                                "gpu_events": round(gt / args.steps * 1e6, 2)}
+            if pct == 1:
+                # roofline of the decode's dominant kernel: algorithmic bytes = received + restored rows
+                rl = roofline_of(rs, ctx, dec, args.profile_steps, (N + L) * S, config, gt / args.steps)
+                decode["roofline_1pct"] = {k: rl[k] for k in ("kernel", "scope", "achieved", "frac", "avg_us",
+                                                              "traffic", "valu_frac", "algorithmic_bytes")}
 
     # ---- a batch of stripes of the same shape per launch (MI355X extension:
     # rs_encode_device_batch / rs_decode_device_batch; one erasure pattern) ----
@@ -201,13 +330,14 @@ def main():
         b_rec = torch.empty((B, M, S), dtype=torch.uint8, device=dev)
         b_out = torch.empty((B, N, S), dtype=torch.uint8, device=dev)
         bsteps = max(5, args.steps // 10)
-        w_e, g_e = timed(lambda: rs.encode_device_batch(N, M, S, b_orig, b_rec, stream=stream, ctx=ctx), bsteps,
-                         max(2, args.warmup // 5))
+        benc = lambda: rs.encode_device_batch(N, M, S, b_orig, b_rec, stream=stream, ctx=ctx)  # noqa: E731
+        w_e = timed(benc, bsteps, max(2, args.warmup // 5))
+        g_e = gpu_time(benc, bsteps, stream)
         L1 = -(-min(N, M) // 100)
         op1 = rs.present_mask([1] * (N - L1) + [0] * L1)
         rp1 = rs.present_mask([1] * L1 + [0] * (M - L1))
-        w_d, _ = timed(lambda: rs.decode_device_batch(N, M, S, b_orig, op1, b_rec, rp1, b_out, stream=stream,
-                                                      ctx=ctx), bsteps, max(2, args.warmup // 5))
+        w_d = timed(lambda: rs.decode_device_batch(N, M, S, b_orig, op1, b_rec, rp1, b_out, stream=stream, ctx=ctx),
+                    bsteps, max(2, args.warmup // 5))
         bbytes = step_bytes * B * world * bsteps
         batched = {"stripes": B, "encode_GiBps": round(bbytes / w_e / 2**30, 3),
                    "encode_us_per_launch": round(g_e / bsteps * 1e6, 2),
@@ -246,27 +376,12 @@ def main():
                     "decode_1pct_GiBps": round(world * step_bytes / ddt / 2**30, 3), "slices": best[0],
                     "note": "pinned host buffers, hipMemcpy2DAsync in + kernels + out, column slices over 3 streams"}
 
-    # ---- device copy for context (STREAM-copy GB/s) ---------
-    copy_ref = None
-    if not args.no_copy:
-        nb = 1 << 30
-        c_src = torch.empty(nb, dtype=torch.uint8, device=dev)
-        c_dst = torch.empty_like(c_src)
-        c_dst.copy_(c_src)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(10):
-            c_dst.copy_(c_src)
-        e1.record()
-        torch.cuda.synchronize()
-        copy_ref = {"GBps": round(2 * nb * 10 / (e0.elapsed_time(e1) / 1e3) / 1e9, 1),
-                    "note": "torch device-to-device copy of 1 GiB (read + write bytes), context for roofline.peak"}
-        del c_src, c_dst
+    copy_ref = None if args.no_copy else device_copy(dev)
 
     # ---- CPU baseline (rank 0, N = 1 only) ----------------------------------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.cpu_seconds)
+        cpu = cpu_baseline(args.cpu_seconds, N, M, S)
 
     if rank == 0:
         line = {
@@ -286,61 +401,65 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
-    if world > 1:
-        dist.destroy_process_group()
 
+
+def device_copy(dev):
+    """A 1 GiB device-to-device copy timed with events: the achievable-bandwidth context
+    for roofline.peak (STREAM-copy GB/s)."""
+    import torch
+
+    nb = 1 << 30
+    c_src = torch.empty(nb, dtype=torch.uint8, device=dev)
+    c_dst = torch.empty_like(c_src)
+    c_dst.copy_(c_src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        c_dst.copy_(c_src)
+    e1.record()
+    torch.cuda.synchronize()
+    return {"GBps": round(2 * nb * 10 / (e0.elapsed_time(e1) / 1e3) / 1e9, 1),
+            "note": "torch device-to-device copy of 1 GiB (read + write bytes), context for roofline.peak"}
+
+
+# ---------------------------------------------------------------------------
+# configs[4]: one 32768:32768 x 64 KiB stripe column-partitioned over the ranks
 
 def sharded_bench(args, rs, ctx, world, rank, dev):
-    """configs[4]: ONE 32768:32768 x 64 KiB stripe column-partitioned over the ranks
-    (DESIGN.md "Multi-GPU"): rank r encodes byte columns
-    [r*w, (r+1)*w), w = 64 KiB / world, of its resident slice of the originals, and an
-    all-gather (RCCL over xGMI) assembles the whole [M x S] recovery matrix on every rank
-    (reed_solomon_simd.encode_device_sharded).  Total work is fixed: strong scaling.
-    Reported: the whole step (encode + all-gather + re-interleave) and encode alone."""
+    """SURVEY.md 8(e), DESIGN.md "Multi-GPU": rank r encodes byte columns [r*w, (r+1)*w),
+    w = 64 KiB / world, of its resident column slice of the originals, and an all-gather (RCCL
+    over xGMI) assembles the whole [M x S] recovery matrix on every rank
+    (reed_solomon_simd.ShardedEncoder).  Total work is fixed: strong scaling.  Reported: the
+    whole step (encode + all-gather + re-interleave) and encode alone."""
     import torch
-    import torch.distributed as dist
 
-    N, M, S = CONFIGS[args.config]
+    N, M, S = CONFIGS[SHARDED]
+    timed, gpu_time = make_timer(world, dev)
+    stream = torch.cuda.current_stream(dev)  # collectives are ordered after this stream's kernels
+    if world > 1:
+        shard = rs.ShardedEncoder(N, M, S, device=dev, stream=stream, ctx=ctx)
     w = S // world
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     d_orig = torch.randint(0, 256, (N, w), dtype=torch.uint8, device=dev, generator=g)  # this rank's columns
     d_rec = torch.empty((M, S), dtype=torch.uint8, device=dev)
-    part = torch.empty((M, w), dtype=torch.uint8, device=dev) if world > 1 else d_rec
-    gathered = torch.empty((world, M, w), dtype=torch.uint8, device=dev) if world > 1 else None
-    cur = torch.cuda.current_stream(dev)  # collectives are ordered after this stream's kernels
-
-    def compute():
-        rs.encode_device(N, M, w, d_orig, part, stream=cur, ctx=ctx)
+    part = shard.part if world > 1 else d_rec
+    compute = rs.encode_device_call(N, M, w, d_orig, part, stream=stream, ctx=ctx)
 
     def step():
         compute()
         if world > 1:
-            dist.all_gather_into_tensor(gathered, part)
-            d_rec.view(M, world, w).copy_(gathered.permute(1, 0, 2))
+            shard.gather(d_rec)
 
-    def timed(fn):
-        for _ in range(args.warmup):
-            fn()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            fn()
-        torch.cuda.synchronize()
-        t = time.perf_counter() - t0
-        if world > 1:
-            dist.barrier()
-        return reduce_max(t, world, dev) / args.steps
-
-    t_step = timed(step)
-    t_comp = timed(compute)
+    t_step = timed(step, args.steps, args.warmup) / args.steps
+    t_comp = timed(compute, args.steps, args.warmup) / args.steps
+    per_gpu = (N + M) * w
+    roofline = roofline_of(rs, ctx, compute, max(3, args.profile_steps // 10), per_gpu, SHARDED)
     total = (N + M) * S
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cpu = cpu_baseline(min(args.cpu_seconds, 10.0), N, M, S)
     if rank == 0:
-        per_gpu = (N + M) * w
-        achieved = per_gpu / t_comp / 1e9
         print(json.dumps({
             "metric": "GiB/s (original+recovery) encode, device-resident, 32768:32768x65536B column-partitioned "
                       "+ RCCL all-gather",
@@ -349,51 +468,49 @@ def sharded_bench(args, rs, ctx, world, rank, dev):
             "scaling": "strong", "vs_baseline": None, "dtype": "u8", "data": "synthetic (uniform random bytes)",
             "config": {"workload": "encode 32768:32768 x 64 KiB (configs[4]), column slice of 64 KiB / n per GPU",
                        "original_count": N, "recovery_count": M, "shard_bytes": S, "slice_bytes": w,
-                       "parallelism": f"column partition x{world} + all_gather_into_tensor"},
-            "encode_only": {"ms_per_step": round(t_comp * 1e3, 4),
-                            "GiBps": round(total / t_comp / 2**30, 3)},
+                       "parallelism": f"column partition x{world} + all_gather_into_tensor (RCCL)"},
+            "encode_only": {"ms_per_step": round(t_comp * 1e3, 4), "GiBps": round(total / t_comp / 2**30, 3)},
             "allgather_and_interleave_ms": round((t_step - t_comp) * 1e3, 4),
-            "roofline": {"bound": "hbm", "kernel": "encode passes (all launches of one slice)",
-                         "scope": "step (all launches)", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                         "algorithmic_bytes": per_gpu},
-            "cpu_baseline": None,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
         }))
 
 
-def load_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/<tag>/traffic.json, written by tools/pmc_traffic.py from
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same bench)."""
-    pdir = os.path.join(ROOT, "profiles")
-    if not os.path.isdir(pdir):
-        return None
-    for tag in sorted(os.listdir(pdir), reverse=True):
-        f = os.path.join(pdir, tag, "traffic.json")
-        if os.path.exists(f):
-            with open(f) as fh:
-                d = json.load(fh)
-            if kernel in d["kernels"]:
-                return {"hbm_bytes": d["kernels"][kernel]["hbm_bytes"], "source": f"profiles/{tag}/traffic.json"}
-    return None
+# ---------------------------------------------------------------------------
+# CPU baseline: the reference's AVX2 engine restated in C (oracle/avx2_port.c)
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or platform.machine()
 
 
-def cpu_baseline(seconds):
-    """AVX2 restatement of the reference engine (oracle/avx2_port.c), 1024:1024 x 1 KiB encode:
-    `value` on 1 thread (the reference is single-threaded); `all_cores` = independent stripes on
-    every host thread this process may use (at most 16, the GPU box's CPU share), an upper bound."""
+def cpu_baseline(seconds, N, M, S):
+    """The AVX2 restatement of the reference engine (oracle/avx2_port.c) on a bounded sample of
+    the workload (shard copy-in + encode, like benches/benchmarks.rs:101-107): `value` on 1 thread
+    (the reference is single-threaded); `all_cores` = independent encodes on every host thread
+    this process may use (at most 16, the GPU box's CPU share), an upper bound.  Large shards
+    are sampled by 64-byte column blocks: every engine op is column-wise, so a 64-B-shard encode
+    is the same work per byte."""
     import threading
 
     import numpy as np
     import oracle_lib as O
 
+    cols = S if N * S <= (64 << 20) else 64
     if O.lib().orc_select_engine(1) != 0:
         return {"value": None, "unit": "GiB/s", "cores": 1, "kind": "port", "sample": "AVX2 unavailable on host"}
-    orig = np.random.default_rng(0).integers(0, 256, (1024, 1024), dtype=np.uint8)
-    O.encode("default", orig, 1024)  # tables built once, before any thread starts
+    orig = np.random.default_rng(0).integers(0, 256, (N, cols), dtype=np.uint8)
+    O.encode("default", orig, M)  # tables built once, before any thread starts
     it, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        O.encode("default", orig, 1024)
+        O.encode("default", orig, M)
         it += 1
     dt = time.perf_counter() - t0
 
@@ -404,7 +521,7 @@ def cpu_baseline(seconds):
     def worker(i):  # ctypes releases the GIL; the oracle's work buffer is thread-local
         mine = orig.copy()
         while time.perf_counter() < stop:
-            O.encode("default", mine, 1024)
+            O.encode("default", mine, M)
             counts[i] += 1
 
     ts = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
@@ -415,11 +532,12 @@ def cpu_baseline(seconds):
         t.join()
     dt_all = time.perf_counter() - t1
     O.lib().orc_select_engine(0)
-    cpu = f"{platform.processor() or platform.machine()}"
-    return {"value": round(2 * 1024 * 1024 * it / dt / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{it} encodes of 1024:1024 x 1024 B in {dt:.1f} s (shard copy-in + encode, like "
-                      f"benches/benchmarks.rs:101-107), single thread, {cpu}",
-            "all_cores": {"value": round(2 * 1024 * 1024 * sum(counts) / dt_all / 2**30, 4), "cores": threads,
+    unit_bytes = (N + M) * cols
+    shape = f"{N}:{M} x {cols} B" + ("" if cols == S else f" (one 64-byte column block of the {S} B shards)")
+    return {"value": round(unit_bytes * it / dt / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{it} encodes of {shape} in {dt:.1f} s (shard copy-in + encode, like "
+                      f"benches/benchmarks.rs:101-107), single thread, {_cpu_model()}",
+            "all_cores": {"value": round(unit_bytes * sum(counts) / dt_all / 2**30, 4), "cores": threads,
                           "sample": f"{sum(counts)} independent encodes on {threads} threads in {dt_all:.1f} s"}}
 
 

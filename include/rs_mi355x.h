@@ -33,8 +33,14 @@
  *   stripes of one shape in one launch)
  *
  * Thread-safety: a context may be shared by threads (like DefaultEngine:
- * Send + Sync, src/lib.rs:385-409); an encoder/decoder handle is used by one
- * thread at a time (like &mut ReedSolomonEncoder).
+ * Send + Sync, src/lib.rs:385-409): calls on one context are serialized on the
+ * host by an internal mutex, and the device scratch is kept per (context,
+ * stream), so calls enqueued on different streams may execute concurrently on
+ * the device.  Do not destroy a stream while calls on it are in flight and
+ * then pass a new stream that reuses its handle.  Every entry point runs on
+ * the context's device and restores the calling thread's current device.  An
+ * encoder/decoder handle is used by one thread at a time (like
+ * &mut ReedSolomonEncoder).
  */
 #ifndef RS_MI355X_H
 #define RS_MI355X_H
@@ -149,8 +155,8 @@ void rs_decoder_free(rs_decoder *dec);
  * row-major with row stride shard_bytes.  shard_bytes must be a positive
  * multiple of 64 (the reference's native block layout, algorithm.md:18-31;
  * other even sizes go through the host API, which re-packs the tail block).
- * Asynchronous on `stream`; scratch is owned by the context (one call in
- * flight per context per stream). */
+ * Asynchronous on `stream` (device scratch per context and stream: see
+ * "Thread-safety" above). */
 rs_status rs_encode_device(rs_context *ctx, rs_rate rate, uint64_t original_count, uint64_t recovery_count,
                            uint64_t shard_bytes, const void *d_original, void *d_recovery, void *stream,
                            rs_error *err);
@@ -220,7 +226,10 @@ rs_status rs_decode_host(rs_context *ctx, rs_rate rate, uint64_t original_count,
 /* ---- Engine trait over a device shard matrix (src/engine.rs:234-291) ----
  * d_rows: shard_count rows of shard_len_64 64-byte blocks (ShardsRefMut,
  * src/engine/shards.rs:100-189).  Infallible in the reference (debug_assert on
- * bad args); here bad args return RS_ERR_INVALID_ARGUMENT. */
+ * bad args); here bad args return RS_ERR_INVALID_ARGUMENT.  Semantics are
+ * engine_naive.rs:43-105 for every row, including rows at and past
+ * truncated_size (only the butterfly groups that start below it are
+ * transformed). */
 rs_status rs_engine_fft(rs_context *ctx, void *d_rows, uint64_t shard_count, uint64_t shard_len_64, uint64_t pos,
                         uint64_t size, uint64_t truncated_size, uint64_t skew_delta, void *stream);
 rs_status rs_engine_ifft(rs_context *ctx, void *d_rows, uint64_t shard_count, uint64_t shard_len_64, uint64_t pos,
@@ -231,6 +240,20 @@ void rs_engine_eval_poly(uint16_t *erasures, uint64_t truncated_size);
 /* formal derivative over all shard_count rows (src/engine/utils.rs:99-104) */
 rs_status rs_engine_formal_derivative(rs_context *ctx, void *d_rows, uint64_t shard_count, uint64_t shard_len_64,
                                       void *stream);
+
+/* ---- Engine trait over a HOST shard array: the reference's own calling convention ----
+ * `rows` is the host storage of a ShardsRefMut (shard_count x shard_len_64 64-byte
+ * blocks, src/engine/shards.rs:100-189); Engine::fft / ifft (src/engine.rs:119-151)
+ * transform rows [pos, pos + size) and Engine::mul (src/engine.rs:154) scales
+ * block_count blocks.  Blocking: the rows are copied to the device, transformed
+ * with the same kernels as rs_engine_fft / rs_engine_ifft / rs_engine_mul, and
+ * copied back.  This is what a Rust `impl Engine` binds; it pays a
+ * PCIe round trip per call, the device-resident calls above do not. */
+rs_status rs_engine_fft_host(rs_context *ctx, uint8_t *rows, uint64_t shard_count, uint64_t shard_len_64,
+                             uint64_t pos, uint64_t size, uint64_t truncated_size, uint64_t skew_delta);
+rs_status rs_engine_ifft_host(rs_context *ctx, uint8_t *rows, uint64_t shard_count, uint64_t shard_len_64,
+                              uint64_t pos, uint64_t size, uint64_t truncated_size, uint64_t skew_delta);
+rs_status rs_engine_mul_host(rs_context *ctx, uint8_t *blocks, uint64_t block_count, uint16_t log_m);
 
 /* ---- kernel timing (bench instrumentation, not a reference item) ----
  * While enabled, every kernel the context launches is bracketed by HIP events

@@ -10,7 +10,9 @@
 
 #include <algorithm>
 #include <cstring>
+#include <memory>
 #include <mutex>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -104,9 +106,56 @@ struct DevBuf {
     }
 };
 
+// Pinned host staging that grows monotonically; `ready` orders its reuse
+// after the asynchronous copy that last read it.
+struct PinnedBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipEvent_t ready = nullptr;
+    uint8_t *get(size_t bytes) {
+        if (ready) check(hipEventSynchronize(ready));  // the previous copy out of it is done
+        if (bytes > cap) {
+            if (p) check(hipHostFree(p));
+            p = nullptr;
+            check(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+            cap = bytes;
+        }
+        return static_cast<uint8_t *>(p);
+    }
+    void copied_on(hipStream_t s) {
+        if (!ready) check(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        check(hipEventRecord(ready, s));
+    }
+    ~PinnedBuf() {
+        if (ready) (void)hipEventSynchronize(ready), (void)hipEventDestroy(ready);
+        if (p) (void)hipHostFree(p);
+    }
+};
+
+// Device scratch of one stream's calls.  Calls on one stream execute in order,
+// so one workspace per (context, stream) makes concurrent calls on different
+// streams safe (rs_mi355x.h "Threading and streams").
 struct Workspace {
     DevBuf buf[4], rowinfo, state;
     std::vector<uint8_t> h_state;
+    PinnedBuf h_state_pinned;  // source of the erasure-state copy of large decodes
+};
+
+// Runs the calling thread on `device` for the scope and restores the thread's
+// previous current device afterwards (the caller's -- e.g. torch's -- device
+// selection is left as it was).
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int device) {
+        check(hipGetDevice(&prev));
+        if (prev != device) check(hipSetDevice(device));
+        else prev = -1;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
 };
 
 }  // namespace
@@ -123,8 +172,15 @@ struct rs_context {
     uint32_t mono_max_packs = 256;   // column kernel only up to this many packs (RS_MI355X_MONO_MAX_PACKS)
     std::mutex img_mu;            // guards d_img
     uint32_t *d_img[13] = {};     // column-kernel twiddle images per L (built on first use)
-    std::mutex mu;  // guards ws (device-resident API scratch)
-    Workspace ws;
+    std::mutex host_engine_mu;  // guards host_engine_buf (rs_engine_*_host staging)
+    DevBuf host_engine_buf;
+    std::mutex mu;  // guards ws_by_stream (device-resident API scratch), prof, recs
+    std::unordered_map<hipStream_t, std::unique_ptr<Workspace>> ws_by_stream;
+    Workspace &ws(hipStream_t s) {  // caller holds mu
+        auto &w = ws_by_stream[s];
+        if (!w) w.reset(new Workspace);
+        return *w;
+    }
     // kernel timing (rs_profile_enable)
     // host-memory pipeline (rs_encode_host / rs_decode_host), built on first use
     struct Pipe {
@@ -265,12 +321,7 @@ void launch(int K, int flags, rs::PassArgs A, uint32_t nsets, uint32_t a, hipStr
     hipEvent_t ev = nullptr;
     if (t_prof_ctx) prof_begin(s, &ev);
     check(rs::launch_pass(K, flags, A, s));
-    if (t_prof_ctx) {
-        static const char *names[4] = {"k_pass_copy", "k_pass_ifft", "k_pass_fft", "k_pass_ifft_fft"};
-        static thread_local char buf[64];
-        snprintf(buf, sizeof buf, "%s<K=%d>", names[flags & 3], K);
-        prof_end(s, ev, buf, pass_bytes(K, A, dec_rd, dec_wr));
-    }
+    if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), pass_bytes(K, A, dec_rd, dec_wr));
 }
 
 // One pass over bit level k of a 2^L-row transform (n rows per chunk).
@@ -330,13 +381,7 @@ void launch_mono(int mode, uint32_t L, const rs::MonoArgs &M, hipStream_t s, uin
     hipEvent_t ev = nullptr;
     if (t_prof_ctx) prof_begin(s, &ev);
     check(rs::launch_mono(mode, int(L), M, s));
-    if (t_prof_ctx) {
-        static thread_local char buf[64];
-        const bool staged = rs::mono_staged(int(L), M.chunks);  // the template's name, as rocprofv3 prints it
-        snprintf(buf, sizeof buf, "k_mono<%u, %d, %d, %s, %s>", L, rs::mono_rows_log2_per_lane(int(L), M.chunks), mode,
-                 staged ? "true" : "false", staged && M.stripes > 1 ? "true" : "false");
-        prof_end(s, ev, buf, bytes);
-    }
+    if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), bytes);
 }
 
 // HighRate encode (rate_high.rs:44-87) from device rows to device rows:
@@ -629,7 +674,10 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
         }
     } else {
         uint8_t *d_state = static_cast<uint8_t *>(ws.state.get(nd));
-        check(hipMemcpyAsync(d_state, st.data(), nd, hipMemcpyHostToDevice, s));
+        uint8_t *h = ws.h_state_pinned.get(nd);
+        std::memcpy(h, st.data(), nd);
+        check(hipMemcpyAsync(d_state, h, nd, hipMemcpyHostToDevice, s));
+        ws.h_state_pinned.copied_on(s);
         E.state = d_state;
     }
     hipEvent_t ev = nullptr;
@@ -876,7 +924,7 @@ rs_status rs_context_create(int device, rs_context **out) {
     auto *ctx = new rs_context;
     ctx->device = device;
     rs_status st = guarded(nullptr, [&]() -> rs_status {
-        check(hipSetDevice(device));
+        DeviceGuard dg(device);
         const rs::GfTables &T = rs::tables();
         check(hipMalloc(&ctx->d_tw, T.perm_by_skew.size() * 4));
         check(hipMalloc(&ctx->d_lut, T.perm_by_log.size() * 4));
@@ -894,6 +942,10 @@ rs_status rs_context_create(int device, rs_context **out) {
         const char *ma = getenv("RS_MI355X_MONO_ALL");
         ctx->mono_all = ma && ma[0] == '1';
         if (const char *mp = getenv("RS_MI355X_MONO_MAX_PACKS")) ctx->mono_max_packs = uint32_t(strtoul(mp, nullptr, 10));
+        // column-kernel twiddle images of every transform size, built now: a lazy
+        // build inside an asynchronous call would stall the device with a
+        // synchronous upload the first time a size is seen
+        for (uint32_t L = kMonoMinL; L <= kMonoMaxL; ++L) mono_images(ctx, L);
         return RS_OK;
     });
     if (st != RS_OK) {
@@ -956,15 +1008,16 @@ rs_status rs_encode_device_strided(rs_context *ctx, rs_rate rate, uint64_t N, ui
     if (S % 64 || !stride_ok(orig_stride, S) || !stride_ok(rec_stride, S)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     return guarded(err, [&]() -> rs_status {
         std::lock_guard<std::mutex> lock(ctx->mu);
+        DeviceGuard dg(ctx->device);
         ProfScope prof(ctx);
         Geom g{S, uint32_t(S / 8)};
         g.orig_stride = orig_stride;
         g.rec_stride = rec_stride;
         auto s = static_cast<hipStream_t>(stream);
         if (high)
-            encode_high(ctx, ctx->ws, g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
+            encode_high(ctx, ctx->ws(s), g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
         else
-            encode_low(ctx, ctx->ws, g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
+            encode_low(ctx, ctx->ws(s), g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
         return set_err(err, RS_OK);
     });
 }
@@ -986,6 +1039,7 @@ rs_status rs_encode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint
     if (stripes == 0) return set_err(err, RS_OK);
     return guarded(err, [&]() -> rs_status {
         std::lock_guard<std::mutex> lock(ctx->mu);
+        DeviceGuard dg(ctx->device);
         ProfScope prof(ctx);
         Geom g{S, uint32_t(S / 8)};
         g.orig_stride = orig_stride;
@@ -998,9 +1052,9 @@ rs_status rs_encode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint
             const uint8_t *o = static_cast<const uint8_t *>(d_orig) + b0 * orig_b;
             uint8_t *r = static_cast<uint8_t *>(d_rec) + b0 * rec_b;
             if (high)
-                encode_high(ctx, ctx->ws, g, N, M, o, r, s);
+                encode_high(ctx, ctx->ws(s), g, N, M, o, r, s);
             else
-                encode_low(ctx, ctx->ws, g, N, M, o, r, s);
+                encode_low(ctx, ctx->ws(s), g, N, M, o, r, s);
         }
         return set_err(err, RS_OK);
     });
@@ -1076,8 +1130,8 @@ rs_status rs_encode_host(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, 
     if (S % 64) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     return guarded(err, [&]() -> rs_status {
         std::lock_guard<std::mutex> lock(ctx->mu);
+        DeviceGuard dg(ctx->device);
         ProfScope prof(ctx);
-        check(hipSetDevice(ctx->device));
         auto &P = pipe_of(ctx);
         auto *d_o = static_cast<uint8_t *>(P.orig.get(N * S));
         auto *d_r = static_cast<uint8_t *>(P.rec.get(M * S));
@@ -1120,8 +1174,8 @@ rs_status rs_decode_host(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, 
     if (have_o == N) return set_err(err, RS_OK);
     return guarded(err, [&]() -> rs_status {
         std::lock_guard<std::mutex> lock(ctx->mu);
+        DeviceGuard dg(ctx->device);
         ProfScope prof(ctx);
-        check(hipSetDevice(ctx->device));
         auto &P = pipe_of(ctx);
         auto *d_o = static_cast<uint8_t *>(P.orig.get(N * S));
         auto *d_r = static_cast<uint8_t *>(P.rec.get(M * S));
@@ -1169,12 +1223,13 @@ rs_status rs_decode_device_strided(rs_context *ctx, rs_rate rate, uint64_t N, ui
     if (have_o == N) return set_err(err, RS_OK);
     return guarded(err, [&]() -> rs_status {
         std::lock_guard<std::mutex> lock(ctx->mu);
+        DeviceGuard dg(ctx->device);
         ProfScope prof(ctx);
         Geom g{S, uint32_t(S / 8)};
         g.orig_stride = orig_stride;
         g.rec_stride = rec_stride;
         g.out_stride = restored_stride;
-        decode_dev(ctx, ctx->ws, high, g, N, M, static_cast<const uint8_t *>(d_orig), orig_present,
+        decode_dev(ctx, ctx->ws(static_cast<hipStream_t>(stream)), high, g, N, M, static_cast<const uint8_t *>(d_orig), orig_present,
                    static_cast<const uint8_t *>(d_rec), rec_present, static_cast<uint8_t *>(d_restored),
                    static_cast<hipStream_t>(stream));
         return set_err(err, RS_OK);
@@ -1211,6 +1266,7 @@ rs_status rs_decode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint
     if (have_o == N || stripes == 0) return set_err(err, RS_OK);
     return guarded(err, [&]() -> rs_status {
         std::lock_guard<std::mutex> lock(ctx->mu);
+        DeviceGuard dg(ctx->device);
         ProfScope prof(ctx);
         Geom g{S, uint32_t(S / 8)};
         g.orig_stride = orig_stride;
@@ -1221,7 +1277,8 @@ rs_status rs_decode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint
         g.out_bstride = restored_stripe_stride ? restored_stripe_stride : N * g.out();
         for (uint64_t b0 = 0; b0 < stripes; b0 += kMaxBatchStripes) {  // grid.y limit
             g.stripes = uint32_t(std::min<uint64_t>(kMaxBatchStripes, stripes - b0));
-            decode_dev(ctx, ctx->ws, high, g, N, M, static_cast<const uint8_t *>(d_orig) + b0 * g.orig_bstride,
+            decode_dev(ctx, ctx->ws(static_cast<hipStream_t>(stream)), high, g, N, M,
+                       static_cast<const uint8_t *>(d_orig) + b0 * g.orig_bstride,
                        orig_present, static_cast<const uint8_t *>(d_rec) + b0 * g.rec_bstride, rec_present,
                        static_cast<uint8_t *>(d_restored) + b0 * g.out_bstride, static_cast<hipStream_t>(stream));
         }
@@ -1280,7 +1337,7 @@ rs_status rs_encoder_encode(rs_encoder *e, rs_error *err) {
         return RS_ERR_TOO_FEW_ORIGINAL_SHARDS;
     }
     return guarded(err, [&]() -> rs_status {
-        check(hipSetDevice(e->ctx->device));
+        DeviceGuard dg(e->ctx->device);
         const Geom g{e->row, uint32_t(e->row / 8)};
         auto *d_orig = static_cast<uint8_t *>(e->d_orig.get(e->N * e->row));
         auto *d_rec = static_cast<uint8_t *>(e->d_rec.get(e->M * e->row));
@@ -1385,7 +1442,7 @@ rs_status rs_decoder_decode(rs_decoder *d, rs_error *err) {
         return set_err(err, RS_OK);
     }
     return guarded(err, [&]() -> rs_status {
-        check(hipSetDevice(d->ctx->device));
+        DeviceGuard dg(d->ctx->device);
         const Geom g{d->row, uint32_t(d->row / 8)};
         auto *d_orig = static_cast<uint8_t *>(d->d_orig.get(d->N * d->row));
         auto *d_rec = static_cast<uint8_t *>(d->d_rec.get(d->M * d->row));
@@ -1492,15 +1549,28 @@ static rs_status engine_xform(rs_context *ctx, void *rows, uint64_t count, uint6
         return RS_ERR_INVALID_ARGUMENT;
     return guarded(nullptr, [&]() -> rs_status {
         std::lock_guard<std::mutex> lock(ctx->mu);
+        DeviceGuard dg(ctx->device);
         const Geom g{len64 * 64, uint32_t(len64 * 8)};
         uint8_t *base = static_cast<uint8_t *>(rows) + pos * g.stride;
         auto s = static_cast<hipStream_t>(stream);
         const uint32_t n = uint32_t(size), L = ilog2(n);
         rs::PassArgs A = base_args(ctx, g, n);
         A.ifft_delta = A.fft_delta = uint32_t(delta);
-        const Levels lv = levels(L, max_k_enc(g.packs));
         A.work_in = A.work_out = base;
         A.work_stride = g.stride;
+        if (trunc < size) {
+            // engine_naive.rs:43-105: each layer transforms only the butterfly groups that
+            // start below truncated_size; rows at and past it keep what the upper layers
+            // left there ("garbage", src/engine.rs:108-147).  One 1-bit pass per layer: the
+            // sets of layer b (dist 2^b) whose group starts below trunc are a prefix.
+            for (uint32_t i = 0; i < L; ++i) {
+                const uint32_t b = fft ? L - 1 - i : i;
+                const uint64_t groups = (trunc + (uint64_t(2) << b) - 1) >> (b + 1);
+                if (groups) launch(1, fft ? rs::kFft : rs::kIfft, A, uint32_t(groups << b), b, s);
+            }
+            return RS_OK;
+        }
+        const Levels lv = levels(L, max_k_enc(g.packs));
         // in place: IFFT runs levels low -> high, FFT high -> low
         for (uint32_t i = 0; i < lv.m; ++i) {
             const uint32_t k = fft ? lv.m - 1 - i : i;
@@ -1523,6 +1593,7 @@ rs_status rs_engine_ifft(rs_context *ctx, void *d_rows, uint64_t shard_count, ui
 rs_status rs_engine_mul(rs_context *ctx, void *d_rows, uint64_t block_count, uint16_t log_m, void *stream) {
     if (!ctx || (!d_rows && block_count)) return RS_ERR_INVALID_ARGUMENT;
     return guarded(nullptr, [&]() -> rs_status {
+        DeviceGuard dg(ctx->device);
         check(rs::launch_mul(static_cast<uint8_t *>(d_rows), block_count, ctx->d_lut + size_t(log_m) * rs::kPermWords,
                              static_cast<hipStream_t>(stream)));
         return RS_OK;
@@ -1534,11 +1605,64 @@ rs_status rs_engine_formal_derivative(rs_context *ctx, void *d_rows, uint64_t co
     if (!ctx || (!d_rows && count) || (count & (count - 1))) return RS_ERR_INVALID_ARGUMENT;
     return guarded(nullptr, [&]() -> rs_status {
         std::lock_guard<std::mutex> lock(ctx->mu);
+        DeviceGuard dg(ctx->device);
         const uint64_t bytes = count * len64 * 64;
-        auto *tmp = static_cast<uint8_t *>(ctx->ws.buf[0].get(bytes));
         auto s = static_cast<hipStream_t>(stream);
+        auto *tmp = static_cast<uint8_t *>(ctx->ws(s).buf[0].get(bytes));
         check(hipMemcpyAsync(tmp, d_rows, bytes, hipMemcpyDeviceToDevice, s));
         check(rs::launch_formal_derivative(tmp, static_cast<uint8_t *>(d_rows), uint32_t(count), len64 * 64, s));
+        return RS_OK;
+    });
+}
+
+// ---- Engine trait over HOST shard arrays (the reference's ShardsRefMut) ----------
+
+namespace {
+// rows [pos, pos + size) of a host array -> device staging -> transform -> back
+rs_status engine_xform_host(rs_context *ctx, uint8_t *rows, uint64_t count, uint64_t len64, uint64_t pos,
+                            uint64_t size, uint64_t trunc, uint64_t delta, bool fft) {
+    if (!ctx || !rows || !len64 || size == 0 || (size & (size - 1)) || pos + size > count || trunc > size ||
+        size > 65536 || delta + size > 65536 + 1)
+        return RS_ERR_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lock(ctx->host_engine_mu);  // the staging buffer, for the whole round trip
+    rs_status st = guarded(nullptr, [&]() -> rs_status {
+        DeviceGuard dg(ctx->device);
+        const uint64_t bytes = size * len64 * 64;
+        void *d = ctx->host_engine_buf.get(bytes);
+        check(hipMemcpy(d, rows + pos * len64 * 64, bytes, hipMemcpyHostToDevice));
+        return RS_OK;
+    });
+    // the device transform on the null stream, between the two blocking copies
+    if (st == RS_OK) st = engine_xform(ctx, ctx->host_engine_buf.p, size, len64, 0, size, trunc, delta, nullptr, fft);
+    if (st != RS_OK) return st;
+    return guarded(nullptr, [&]() -> rs_status {
+        DeviceGuard dg(ctx->device);
+        check(hipMemcpy(rows + pos * len64 * 64, ctx->host_engine_buf.p, size * len64 * 64, hipMemcpyDeviceToHost));
+        return RS_OK;
+    });
+}
+}  // namespace
+
+rs_status rs_engine_fft_host(rs_context *ctx, uint8_t *rows, uint64_t shard_count, uint64_t shard_len_64,
+                             uint64_t pos, uint64_t size, uint64_t truncated_size, uint64_t skew_delta) {
+    return engine_xform_host(ctx, rows, shard_count, shard_len_64, pos, size, truncated_size, skew_delta, true);
+}
+rs_status rs_engine_ifft_host(rs_context *ctx, uint8_t *rows, uint64_t shard_count, uint64_t shard_len_64,
+                              uint64_t pos, uint64_t size, uint64_t truncated_size, uint64_t skew_delta) {
+    return engine_xform_host(ctx, rows, shard_count, shard_len_64, pos, size, truncated_size, skew_delta, false);
+}
+rs_status rs_engine_mul_host(rs_context *ctx, uint8_t *blocks, uint64_t block_count, uint16_t log_m) {
+    if (!ctx || (!blocks && block_count)) return RS_ERR_INVALID_ARGUMENT;
+    if (!block_count) return RS_OK;
+    return guarded(nullptr, [&]() -> rs_status {
+        std::lock_guard<std::mutex> lock(ctx->host_engine_mu);
+        DeviceGuard dg(ctx->device);
+        const uint64_t bytes = block_count * 64;
+        void *d = ctx->host_engine_buf.get(bytes);
+        check(hipMemcpy(d, blocks, bytes, hipMemcpyHostToDevice));
+        check(rs::launch_mul(static_cast<uint8_t *>(d), block_count, ctx->d_lut + size_t(log_m) * rs::kPermWords,
+                             nullptr));
+        check(hipMemcpy(blocks, d, bytes, hipMemcpyDeviceToHost));
         return RS_OK;
     });
 }
@@ -1561,7 +1685,7 @@ rs_status rs_mono_enable(rs_context *ctx, int enable) {
 rs_status rs_check_device(rs_context *ctx) {
     if (!ctx) return RS_ERR_INVALID_ARGUMENT;
     return guarded(nullptr, [&]() -> rs_status {
-        check(hipSetDevice(ctx->device));
+        DeviceGuard dg(ctx->device);
         check(hipDeviceSynchronize());
         check(hipGetLastError());
         return RS_OK;

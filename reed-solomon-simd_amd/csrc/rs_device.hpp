@@ -79,6 +79,12 @@ enum PassFlags {
 // Launch one pass on `stream`.  K = log2(rows per set).
 hipError_t launch_pass(int K, int flags, const PassArgs &args, hipStream_t stream);
 
+// Name of the kernel the last launch_pass / launch_mono call of this thread
+// launched, in rocprofv3's short form ("k_pass<8, 3, 4, 1>"): the profiler's
+// records (rs_profile_collect) and the committed PMC summaries share it.
+constexpr int kLaunchNameBytes = 96;
+char *launch_name_buf();
+
 // Column kernel (DESIGN.md "Column kernel"): one workgroup owns ALL n = 2^L
 // transform rows of one pack (4 elements of every row), so a whole encode or
 // decode runs without any cross-workgroup exchange.  Twiddles come from

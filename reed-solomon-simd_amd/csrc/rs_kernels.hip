@@ -15,6 +15,7 @@
 // of a pass are staged in LDS once per workgroup.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <type_traits>
 
 #include "rs_device.hpp"
@@ -724,6 +725,7 @@ hipError_t launch_f(const PassArgs &A, hipStream_t s) {
     B.slices = (A.packs + P::SP - 1) / P::SP;
     dim3 grid(B.slices * B.nsets, B.grid_chunks);
     k_pass<K, LR, SPL, F><<<grid, P::kThreads, lds, s>>>(B);
+    snprintf(launch_name_buf(), kLaunchNameBytes, "k_pass<%d, %d, %d, %d>", K, LR, SPL, F);
     return hipGetLastError();
 }
 
@@ -797,6 +799,11 @@ __global__ void k_formal_derivative(const uint8_t *in, uint8_t *out, uint32_t ro
 }
 
 }  // namespace
+
+char *launch_name_buf() {
+    static thread_local char name[kLaunchNameBytes];
+    return name;
+}
 
 hipError_t launch_pass(int K, int flags, const PassArgs &A, hipStream_t s) {
     // narrow slices when the wide shape's slices leave the chip under-filled

@@ -23,6 +23,8 @@
 // butterflies of the current layer.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+
 #include "rs_device.hpp"
 #include "rs_gf.hpp"
 
@@ -1109,6 +1111,8 @@ hipError_t launch_ls(const MonoArgs &A, hipStream_t s) {
     }
     const uint32_t grid = 8u * A.packs_per_xcd;
     k_mono<L, LR, MODE, STAGED, BATCH><<<dim3(grid, BATCH ? A.stripes : 1), 1 << (L - LR), lds, s>>>(A);
+    snprintf(launch_name_buf(), kLaunchNameBytes, "k_mono<%d, %d, %d, %s, %s>", L, LR, MODE, STAGED ? "true" : "false",
+             BATCH ? "true" : "false");
     return hipGetLastError();
 }
 

@@ -100,6 +100,9 @@ _sig("rs_engine_ifft", _int, _vp, _vp, _u64, _u64, _u64, _u64, _u64, _u64, _vp)
 _sig("rs_engine_mul", _int, _vp, _vp, _u64, ctypes.c_uint16, _vp)
 _sig("rs_engine_eval_poly", None, ctypes.POINTER(ctypes.c_uint16), _u64)
 _sig("rs_engine_formal_derivative", _int, _vp, _vp, _u64, _u64, _vp)
+_sig("rs_engine_fft_host", _int, _vp, _vp, _u64, _u64, _u64, _u64, _u64, _u64)
+_sig("rs_engine_ifft_host", _int, _vp, _vp, _u64, _u64, _u64, _u64, _u64, _u64)
+_sig("rs_engine_mul_host", _int, _vp, _vp, _u64, ctypes.c_uint16)
 for _t in ("exp", "log", "skew", "log_walsh"):
     _sig(f"rs_table_{_t}", ctypes.POINTER(ctypes.c_uint16))
 for _t in ("perm_by_log", "perm_by_skew"):
@@ -621,6 +624,29 @@ def _row_stride(x) -> int:
     return 0
 
 
+def _check_matrix(x, rows: int, shard_bytes: int, what: str, dims: int = 2, on_device: bool = True) -> None:
+    """A tensor argument must be a uint8 device tensor [.., >= rows, shard_bytes]: the kernels
+    address rows * stride bytes, so an undersized tensor would be written past its end (the
+    reference rejects wrong sizes with DifferentShardSize).  Raw pointers are the caller's
+    responsibility."""
+    if not hasattr(x, "data_ptr"):
+        return
+    if str(x.dtype) != "torch.uint8":
+        raise ValueError(f"{what}: dtype must be uint8, got {x.dtype}")
+    if on_device and not x.is_cuda:
+        raise ValueError(f"{what}: must be a device (cuda/HIP) tensor")
+    if x.dim() != dims:
+        raise ValueError(f"{what}: expected a {dims}-D tensor, got shape {tuple(x.shape)}")
+    if x.shape[-2] < rows or x.shape[-1] != shard_bytes:
+        raise ValueError(f"{what}: shape {tuple(x.shape)} does not hold {rows} rows of {shard_bytes} bytes")
+
+
+def _check_mask(mask: bytes, count: int, what: str) -> bytes:
+    if len(mask) != count:
+        raise ValueError(f"{what}: {len(mask)} flags for {count} shards")
+    return mask
+
+
 def encode_device(original_count: int, recovery_count: int, shard_bytes: int, d_original, d_recovery,
                   stream=None, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None) -> None:
     """Encode shard matrices resident in device memory (rs_encode_device[_strided]).
@@ -628,6 +654,8 @@ def encode_device(original_count: int, recovery_count: int, shard_bytes: int, d_
     d_original / d_recovery: torch uint8 tensors [count, shard_bytes] (column-slice views of wider
     matrices allowed) or raw device pointers to contiguous rows."""
     ctx = ctx or default_context()
+    _check_matrix(d_original, original_count, shard_bytes, "d_original")
+    _check_matrix(d_recovery, recovery_count, shard_bytes, "d_recovery")
     err = _RsError()
     _raise(_lib.rs_encode_device_strided(ctx.handle, rate_, original_count, recovery_count, shard_bytes,
                                          _ptr(d_original), _row_stride(d_original), _ptr(d_recovery),
@@ -647,6 +675,8 @@ def encode_device_batch(original_count: int, recovery_count: int, shard_bytes: i
     """Encode a batch of stripes of one shape (rs_encode_device_batch): d_original
     [stripes, original_count, shard_bytes], d_recovery [stripes, recovery_count, shard_bytes]."""
     ctx = ctx or default_context()
+    _check_matrix(d_original, original_count, shard_bytes, "d_original", 3)
+    _check_matrix(d_recovery, recovery_count, shard_bytes, "d_recovery", 3)
     if d_original.shape[0] != d_recovery.shape[0]:
         raise ValueError("original and recovery batches differ in stripe count")
     (o_row, o_b), (r_row, r_b) = _batch_strides(d_original), _batch_strides(d_recovery)
@@ -662,6 +692,9 @@ def decode_device_batch(original_count: int, recovery_count: int, shard_bytes: i
     """Decode a batch of stripes sharing ONE erasure pattern (rs_decode_device_batch); tensors
     [stripes, rows, shard_bytes]; only missing originals of d_restored are written."""
     ctx = ctx or default_context()
+    _check_matrix(d_original, original_count, shard_bytes, "d_original", 3)
+    _check_matrix(d_recovery, recovery_count, shard_bytes, "d_recovery", 3)
+    _check_matrix(d_restored, original_count, shard_bytes, "d_restored", 3)
     n = d_original.shape[0]
     if d_recovery.shape[0] != n or d_restored.shape[0] != n:
         raise ValueError("batches differ in stripe count")
@@ -669,8 +702,10 @@ def decode_device_batch(original_count: int, recovery_count: int, shard_bytes: i
                                                 _batch_strides(d_restored))
     err = _RsError()
     _raise(_lib.rs_decode_device_batch(ctx.handle, rate_, original_count, recovery_count, shard_bytes, n,
-                                       d_original.data_ptr(), o_row, o_b, present_mask(original_present),
-                                       d_recovery.data_ptr(), r_row, r_b, present_mask(recovery_present),
+                                       d_original.data_ptr(), o_row, o_b,
+                                       _check_mask(present_mask(original_present), original_count, "original_present"),
+                                       d_recovery.data_ptr(), r_row, r_b,
+                                       _check_mask(present_mask(recovery_present), recovery_count, "recovery_present"),
                                        d_restored.data_ptr(), x_row, x_b, _stream(stream), ctypes.byref(err)), err)
 
 
@@ -687,8 +722,11 @@ def decode_device(original_count: int, recovery_count: int, shard_bytes: int, d_
                   d_recovery, recovery_present, d_restored, stream=None, rate_: int = RATE_DEFAULT,
                   ctx: Optional[Context] = None) -> None:
     ctx = ctx or default_context()
-    op = present_mask(original_present)
-    rp = present_mask(recovery_present)
+    op = _check_mask(present_mask(original_present), original_count, "original_present")
+    rp = _check_mask(present_mask(recovery_present), recovery_count, "recovery_present")
+    _check_matrix(d_original, original_count, shard_bytes, "d_original")
+    _check_matrix(d_recovery, recovery_count, shard_bytes, "d_recovery")
+    _check_matrix(d_restored, original_count, shard_bytes, "d_restored")
     err = _RsError()
     _raise(_lib.rs_decode_device_strided(ctx.handle, rate_, original_count, recovery_count, shard_bytes,
                                          _ptr(d_original), _row_stride(d_original), op, _ptr(d_recovery),
@@ -721,6 +759,8 @@ def encode_device_call(original_count: int, recovery_count: int, shard_bytes: in
                        stream=None, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None) -> DeviceCall:
     """encode_device(...) bound once; call the result to encode."""
     ctx = ctx or default_context()
+    _check_matrix(d_original, original_count, shard_bytes, "d_original")
+    _check_matrix(d_recovery, recovery_count, shard_bytes, "d_recovery")
     u = ctypes.c_uint64
     args = (_vp(ctx.handle.value), _int(rate_), u(original_count), u(recovery_count), u(shard_bytes),
             _vp(_ptr(d_original)), u(_row_stride(d_original)), _vp(_ptr(d_recovery)), u(_row_stride(d_recovery)),
@@ -733,8 +773,11 @@ def decode_device_call(original_count: int, recovery_count: int, shard_bytes: in
                        ctx: Optional[Context] = None) -> DeviceCall:
     """decode_device(...) bound once; call the result to decode."""
     ctx = ctx or default_context()
-    op = present_mask(original_present)
-    rp = present_mask(recovery_present)
+    op = _check_mask(present_mask(original_present), original_count, "original_present")
+    rp = _check_mask(present_mask(recovery_present), recovery_count, "recovery_present")
+    _check_matrix(d_original, original_count, shard_bytes, "d_original")
+    _check_matrix(d_recovery, recovery_count, shard_bytes, "d_recovery")
+    _check_matrix(d_restored, original_count, shard_bytes, "d_restored")
     u = ctypes.c_uint64
     args = (_vp(ctx.handle.value), _int(rate_), u(original_count), u(recovery_count), u(shard_bytes),
             _vp(_ptr(d_original)), u(_row_stride(d_original)), op, _vp(_ptr(d_recovery)),
@@ -780,50 +823,97 @@ def decode_host(original_count: int, recovery_count: int, shard_bytes: int, h_or
     ctx = ctx or default_context()
     err = _RsError()
     _raise(_lib.rs_decode_host(ctx.handle, rate_, original_count, recovery_count, shard_bytes,
-                               _host_ptr(h_original), present_mask(original_present), _host_ptr(h_recovery),
-                               present_mask(recovery_present), _host_ptr(h_restored), slices,
+                               _host_ptr(h_original),
+                               _check_mask(present_mask(original_present), original_count, "original_present"),
+                               _host_ptr(h_recovery),
+                               _check_mask(present_mask(recovery_present), recovery_count, "recovery_present"),
+                               _host_ptr(h_restored), slices,
                                ctypes.byref(err)), err)
 
 
-def _sharded_encode(original_count, recovery_count, shard_bytes, d_original, d_recovery, encode_slice, group=None):
-    """Column-partitioned encode over the ranks of `group`.
+class ShardedEncoder:
+    """Column-partitioned encode of ONE stripe over the ranks of a process group, one GPU per
+    rank.  Rank r owns byte columns [r*w, (r+1)*w) of every shard,
+    w = shard_bytes / world (whole 64-byte blocks); it encodes them on its device
+    (rs_encode_device_strided) into a [recovery_count x w] slice, and an all-gather (RCCL over
+    xGMI for the "nccl" backend) plus a re-interleave assembles the whole [recovery_count x
+    shard_bytes] recovery matrix on every rank.  Every engine op is column-wise, so the result
+    equals a single-device encode.  The slice and gather buffers are allocated once per
+    encoder.  `encode_slice(orig_cols, rec_slice)` replaces the per-slice device encode (tests
+    drive this plumbing on CPU with a stand-in)."""
 
-    Rank r encodes byte columns [r*w, (r+1)*w), w = shard_bytes / world (whole 64-byte blocks),
-    with encode_slice(orig_cols_view, rec_slice); the [M x w] recovery slices are all-gathered
-    (RCCL over xGMI for the "nccl" backend) and re-interleaved into d_recovery [M x S] on every
-    rank.  Every engine op is column-wise, so the result equals a single-device encode."""
-    import torch
-    import torch.distributed as dist
+    def __init__(self, original_count: int, recovery_count: int, shard_bytes: int, device=None, group=None,
+                 stream=None, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None, encode_slice=None):
+        import torch
+        import torch.distributed as dist
 
-    world, rank = dist.get_world_size(group), dist.get_rank(group)
-    if shard_bytes % (64 * world):
-        raise ValueError(f"shard_bytes {shard_bytes} must split into whole 64-byte blocks over {world} ranks")
-    w = shard_bytes // world
-    part = torch.empty((recovery_count, w), dtype=torch.uint8, device=d_recovery.device)
-    encode_slice(d_original[:, rank * w:(rank + 1) * w], part)
-    if dist.get_backend(group) == "nccl":
-        gathered = torch.empty((world, recovery_count, w), dtype=torch.uint8, device=d_recovery.device)
-        dist.all_gather_into_tensor(gathered, part, group=group)
-    else:
-        pieces = [torch.empty_like(part) for _ in range(world)]
-        dist.all_gather(pieces, part, group=group)
-        gathered = torch.stack(pieces)
-    d_recovery.view(recovery_count, world, w).copy_(gathered.permute(1, 0, 2))
+        self.group = group
+        self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        if shard_bytes % (64 * self.world):
+            raise ValueError(f"shard_bytes {shard_bytes} must split into whole 64-byte blocks over "
+                             f"{self.world} ranks")
+        self.N, self.M, self.S = original_count, recovery_count, shard_bytes
+        self.w = shard_bytes // self.world
+        self.stream, self.rate, self.ctx = stream, rate_, ctx
+        self._encode_slice = encode_slice
+        self.nccl = dist.get_backend(group) == "nccl"
+        dev = torch.device(device) if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if self.nccl else torch.device("cpu"))
+        self.part = torch.empty((recovery_count, self.w), dtype=torch.uint8, device=dev)
+        self.gathered = (torch.empty((self.world, recovery_count, self.w), dtype=torch.uint8, device=dev)
+                         if self.world > 1 else None)
+
+    def columns(self, d_original):
+        """This rank's column slice of a full [N x S] original matrix (a strided view)."""
+        return d_original[:, self.rank * self.w:(self.rank + 1) * self.w]
+
+    def encode_local(self, orig_cols) -> None:
+        """Encode this rank's [N x w] columns into self.part."""
+        if self._encode_slice is not None:
+            self._encode_slice(orig_cols, self.part)
+            return
+        encode_device(self.N, self.M, self.w, orig_cols, self.part, stream=self.stream, rate_=self.rate,
+                      ctx=self.ctx)
+        if self.stream is not None:
+            import torch
+            torch.cuda.current_stream().wait_stream(self.stream)  # collectives run on the current stream
+
+    def gather(self, d_recovery) -> None:
+        """All-gather every rank's slice and re-interleave into d_recovery [M x S]."""
+        import torch.distributed as dist
+
+        if self.world == 1:
+            d_recovery.copy_(self.part)
+            return
+        if self.nccl:
+            dist.all_gather_into_tensor(self.gathered, self.part, group=self.group)
+        else:
+            dist.all_gather(list(self.gathered.unbind(0)), self.part, group=self.group)
+        d_recovery.view(self.M, self.world, self.w).copy_(self.gathered.permute(1, 0, 2))
+
+    def __call__(self, orig_cols, d_recovery) -> None:
+        self.encode_local(orig_cols)
+        self.gather(d_recovery)
+
+
+_sharded_cache: Dict[tuple, ShardedEncoder] = {}
 
 
 def encode_device_sharded(original_count: int, recovery_count: int, shard_bytes: int, d_original, d_recovery,
                           group=None, stream=None, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None) -> None:
     """Multi-GPU encode of one large stripe: each rank (one GPU each) encodes its column slice of
-    d_original [N x S] on its device, then an all-gather assembles d_recovery [M x S] everywhere."""
-    import torch
-
-    def enc(orig_cols, rec_slice):
-        encode_device(original_count, recovery_count, orig_cols.shape[1], orig_cols, rec_slice,
-                      stream=stream, rate_=rate_, ctx=ctx)
-        if stream is not None:
-            torch.cuda.current_stream().wait_stream(stream)
-
-    _sharded_encode(original_count, recovery_count, shard_bytes, d_original, d_recovery, enc, group)
+    d_original [N x S] on its device, then an all-gather assembles d_recovery [M x S] everywhere
+    (ShardedEncoder, cached per shape / group / device)."""
+    key = (original_count, recovery_count, shard_bytes, id(group), str(d_recovery.device), _stream(stream), rate_,
+           id(ctx))
+    enc = _sharded_cache.get(key)
+    if enc is None:
+        enc = _sharded_cache[key] = ShardedEncoder(original_count, recovery_count, shard_bytes,
+                                                   device=d_recovery.device, group=group, stream=stream,
+                                                   rate_=rate_, ctx=ctx)
+    _check_matrix(d_recovery, recovery_count, shard_bytes, "d_recovery", on_device=False)
+    _check_matrix(d_original, original_count, shard_bytes, "d_original", on_device=False)
+    enc(enc.columns(d_original), d_recovery)
 
 
 class engine:
@@ -853,6 +943,25 @@ class engine:
         ctx = ctx or default_context()
         _raise(_lib.rs_engine_formal_derivative(ctx.handle, _ptr(d_rows), shard_count, shard_len_64,
                                                 _stream(stream)), _RsError())
+
+    # the same ops on a HOST array (numpy uint8 [shard_count, shard_len_64 * 64], C-contiguous,
+    # writable), the reference's own calling convention (rs_engine_*_host; blocking)
+    @staticmethod
+    def fft_host(rows, shard_count, shard_len_64, pos, size, truncated_size, skew_delta, ctx=None):
+        ctx = ctx or default_context()
+        _raise(_lib.rs_engine_fft_host(ctx.handle, _host_ptr(rows), shard_count, shard_len_64, pos, size,
+                                       truncated_size, skew_delta), _RsError())
+
+    @staticmethod
+    def ifft_host(rows, shard_count, shard_len_64, pos, size, truncated_size, skew_delta, ctx=None):
+        ctx = ctx or default_context()
+        _raise(_lib.rs_engine_ifft_host(ctx.handle, _host_ptr(rows), shard_count, shard_len_64, pos, size,
+                                        truncated_size, skew_delta), _RsError())
+
+    @staticmethod
+    def mul_host(blocks, block_count, log_m, ctx=None):
+        ctx = ctx or default_context()
+        _raise(_lib.rs_engine_mul_host(ctx.handle, _host_ptr(blocks), block_count, log_m), _RsError())
 
     @staticmethod
     def eval_poly(erasures, truncated_size):

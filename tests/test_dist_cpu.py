@@ -1,10 +1,14 @@
-"""Multi-rank plumbing on CPU (gloo, world_size 2, 127.0.0.1).
+"""Multi-rank plumbing on CPU (gloo, 127.0.0.1).
 
 - Column-partitioned encode: the product's
-  `_sharded_encode` (partition into whole 64-byte blocks, all-gather,
-  re-interleave) with the CPU oracle injected as the per-rank slice encoder
-  -- on the GPU the slice encoder is rs_encode_device_strided.
-- bench.py's max-over-ranks timing reduction.
+  `encode_device_sharded` / `ShardedEncoder` (partition into whole 64-byte
+  blocks, per-rank slice encode, all-gather, re-interleave), world sizes 2 and
+  4.  Only the per-slice device call (`encode_device` = rs_encode_device_strided
+  on the GPU) is replaced by a CPU stand-in (the oracle); everything around it
+  is the product code.
+- bench.py's max-over-ranks timing reduction, and its `--gpus N` launcher:
+  the parent process starts N ranks (torch.distributed.run) and rank 0 reports
+  n_gpus = the process group's world size.
 """
 import os
 import socket
@@ -37,17 +41,25 @@ def _worker_sharded(rank, world, port, N, M, S, rate, q):
     import oracle_lib as O
     import reed_solomon_simd as rs
     _init(rank, world, port)
+    calls = []
+
+    def slice_standin(n, m, w, cols, out, stream=None, rate_=0, ctx=None):
+        # CPU stand-in for rs_encode_device_strided on this rank's column slice
+        assert (n, m, w) == (N, M, S // world) and cols.shape == (N, w) and out.shape == (M, w)
+        calls.append(w)
+        out.copy_(torch.from_numpy(O.encode(rate, np.ascontiguousarray(cols.numpy()), m)))
+
+    rs.encode_device = slice_standin
     try:
         orig = O.generate_original(N, S, 21)
         d_orig = torch.from_numpy(orig)
-        d_rec = torch.zeros((M, S), dtype=torch.uint8)
-
-        def enc_slice(cols, out):
-            out.copy_(torch.from_numpy(O.encode(rate, np.ascontiguousarray(cols.numpy()), M)))
-
-        rs._sharded_encode(N, M, S, d_orig, d_rec, enc_slice)
         want = O.encode(rate, orig, M)
-        q.put((rank, bool(np.array_equal(d_rec.numpy(), want))))
+        ok = True
+        for _ in range(2):  # second call reuses the cached ShardedEncoder's buffers
+            d_rec = torch.zeros((M, S), dtype=torch.uint8)
+            rs.encode_device_sharded(N, M, S, d_orig, d_rec, rate_={"high": 1, "low": 2}[rate])
+            ok = ok and bool(np.array_equal(d_rec.numpy(), want))
+        q.put((rank, (ok, len(calls), len(rs._sharded_cache))))
     finally:
         dist.destroy_process_group()
 
@@ -77,12 +89,28 @@ def _spawn(fn, world, *args):
     return out
 
 
-@pytest.mark.parametrize("N,M,S,rate", [(64, 64, 256, "high"), (100, 300, 512, "low"), (1000, 1000, 128, "high")])
-def test_column_partitioned_encode_world2(N, M, S, rate):
-    out = _spawn(_worker_sharded, 2, N, M, S, rate)
-    assert out == {0: True, 1: True}
+@pytest.mark.parametrize("world,N,M,S,rate", [(2, 64, 64, 256, "high"), (2, 100, 300, 512, "low"),
+                                              (2, 1000, 1000, 128, "high"), (4, 300, 200, 1024, "high")])
+def test_column_partitioned_encode(world, N, M, S, rate):
+    out = _spawn(_worker_sharded, world, N, M, S, rate)
+    assert out == {r: (True, 2, 1) for r in range(world)}
 
 
 def test_bench_max_over_ranks_world2():
     out = _spawn(_worker_reduce, 2)
     assert out == {0: 2.5, 1: 2.5}
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`python bench.py --gpus 2` from a plain parent starts 2 ranks; --plumbing runs the rank
+    set-up, barriers and max-over-ranks timing on gloo without touching a GPU."""
+    import json
+    import subprocess
+    import sys
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--plumbing", "--steps", "3",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    assert lines[0]["n_gpus"] == 2 and lines[0]["ranks_seen"] == [0, 1] and lines[0]["steps"] == 3

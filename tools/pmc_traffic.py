@@ -1,14 +1,17 @@
 #!/usr/bin/env python3
 """Summarise a gpu_round.sh run into profiles/<tag>/.
 
-Reads gpurun_out/<tag>/{kt,pmc_fetch,pmc_write} (rocprofv3 CSV output) and
-writes
-  profiles/<tag>/kernel_stats.csv   -- rocprofv3 --kernel-trace --stats summary
-  profiles/<tag>/traffic.json       -- per-kernel average HBM-side bytes per launch
-  profiles/<tag>/bench.json         -- the bench line of the same session
+Reads gpurun_out/<tag>/ (rocprofv3 CSV output of tools/gpu_round.sh) and writes
+  profiles/<tag>/kernel_stats.csv       -- rocprofv3 --kernel-trace --stats summary (headline bench)
+  profiles/<tag>/kernel_stats_<cfg>.csv -- the same for the other configs' benches, when run
+  profiles/<tag>/traffic.json           -- per config and kernel: average HBM-side bytes and VALU
+                                           wave-instructions per launch
+  profiles/<tag>/sq_<cfg>.csv           -- the raw SQ counter pass of each config
+  profiles/<tag>/bench*.json            -- the bench lines of the same session
 HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md "HBM": FETCH_SIZE and
 WRITE_SIZE (KiB) come from separate --pmc passes; on gfx950 FETCH_SIZE counts
-half the bytes of a streaming read, so it is doubled.
+half the bytes of a streaming read, so it is doubled.  SQ_INSTS_VALU (a third
+pass with the other SQ counters) is the sum over all waves of a dispatch.
 """
 import collections
 import csv
@@ -19,6 +22,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADLINE = "1024x1024x1k"
 
 
 def short(name):
@@ -29,6 +33,8 @@ def short(name):
 
 def counter_means(path, counter):
     acc = collections.defaultdict(list)
+    if not os.path.exists(path):
+        return {}
     with open(path) as f:
         for r in csv.DictReader(f):
             if r["Counter_Name"] == counter:
@@ -36,34 +42,57 @@ def counter_means(path, counter):
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
 
+def summarise(d):
+    """d: directory holding fetch/, write/, sq/ rocprofv3 outputs of one bench command."""
+    fetch = counter_means(os.path.join(d, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = counter_means(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+    sq = os.path.join(d, "sq", "run_counter_collection.csv")
+    valu = counter_means(sq, "SQ_INSTS_VALU")
+    out = {}
+    for k in sorted(set(fetch) | set(valu)):
+        if not k.startswith("k_"):
+            continue
+        e = {}
+        if k in fetch and k in write:
+            fb = fetch[k][0] * 1024 * 2  # KiB, gfx950 half-count correction
+            wb = write[k][0] * 1024
+            e.update(fetch_bytes=round(fb), write_bytes=round(wb), hbm_bytes=round(fb + wb), launches=fetch[k][1])
+        if k in valu:
+            e.update(valu_insts=round(valu[k][0]), valu_launches=valu[k][1])
+        out[k] = e
+    return out
+
+
 def main(tag):
     src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
-    shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
-    for f in ("bench.json", "bench_config3.json", "bench_config4.json", "bench_config5_n1.json"):
-        if os.path.exists(os.path.join(src, f)) and os.path.getsize(os.path.join(src, f)):
+    for f in sorted(os.listdir(src)):
+        if f.startswith("bench") and f.endswith(".json") and os.path.getsize(os.path.join(src, f)):
             shutil.copy(os.path.join(src, f), os.path.join(dst, f))
-    fetch = counter_means(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-    write = counter_means(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
-    out = {}
-    for k in sorted(set(fetch) & set(write)):
-        if not k.startswith("k_"):
-            continue
-        fb = fetch[k][0] * 1024 * 2  # KiB, gfx950 half-count correction
-        wb = write[k][0] * 1024
-        out[k] = {"fetch_bytes": round(fb), "write_bytes": round(wb), "hbm_bytes": round(fb + wb),
-                  "launches": fetch[k][1]}
+    configs = {}
+    pmc = os.path.join(src, "pmc")
+    for cfg in sorted(os.listdir(pmc)) if os.path.isdir(pmc) else []:
+        configs[cfg] = summarise(os.path.join(pmc, cfg))
+        sq = os.path.join(pmc, cfg, "sq", "run_counter_collection.csv")
+        if os.path.exists(sq):
+            shutil.copy(sq, os.path.join(dst, f"sq_{cfg}.csv"))
+    kt = os.path.join(src, "kt")
+    for cfg in sorted(os.listdir(kt)) if os.path.isdir(kt) else []:
+        f = os.path.join(kt, cfg, "run_kernel_stats.csv")
+        if os.path.exists(f):
+            shutil.copy(f, os.path.join(dst, "kernel_stats.csv" if cfg == HEADLINE else f"kernel_stats_{cfg}.csv"))
     with open(os.path.join(dst, "traffic.json"), "w") as f:
-        json.dump({"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes ({tag})",
-                   "correction": "FETCH_SIZE x2 (gfx950 half count; calibrated for the column kernel's 4-byte paired-lane "
-                                 "pack reads by tools/fetch_calib.hip, profiles/r01j/fetch_calib_*.csv: a 512 MiB read "
-                                 "reports 262,155 KiB, the 16 B/lane stream 262,147 KiB), KiB -> bytes",
-                   "note": "FETCH counts L2 misses per XCD (Infinity-Cache hits included): tables read by every "
-                           "workgroup are fetched once per XCD, 8x their size",
-                   "kernels": out}, f, indent=1)
-    print(json.dumps(out, indent=1))
+        json.dump({"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ counters, separate passes per bench "
+                             f"config ({tag})",
+                   "correction": "FETCH_SIZE x2 (gfx950 half count; calibrated for the column kernel's 4-byte "
+                                 "paired-lane pack reads by tools/fetch_calib.hip, profiles/r01j/fetch_calib_*.csv: "
+                                 "a 512 MiB read reports 262,155 KiB, the 16 B/lane stream 262,147 KiB), KiB -> bytes",
+                   "note": "FETCH counts L2 misses per XCD (Infinity-Cache hits included); valu_insts = SQ_INSTS_VALU "
+                           "per launch, summed over all waves",
+                   "configs": configs, "kernels": configs.get(HEADLINE, {})}, f, indent=1)
+    print(json.dumps(configs, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    main(sys.argv[1] if len(sys.argv) > 1 else "r02")
