@@ -278,7 +278,9 @@ rs_status rs_check_device(rs_context *ctx);
  * the pass kernels instead (also: RS_MI355X_NO_MONO=1 at context
  * creation); 1 (default) uses it where it is fastest (single-chunk transforms
  * of 2^7 .. 2^10 rows, twiddles staged in LDS); 2 also for multi-chunk and
- * 2^11 / 2^12-row transforms (also: RS_MI355X_MONO_ALL=1). */
+ * 2^11 / 2^12-row transforms (also: RS_MI355X_MONO_ALL=1).  Adding 4 turns off
+ * the split decode plan of 2^9 .. 2^11-row decodes whose restored rows lie in
+ * one half of the work rows (also: RS_MI355X_NO_SPLIT=1); A/B and tests. */
 rs_status rs_mono_enable(rs_context *ctx, int enable);
 
 /* ---- GF(2^16) tables (src/engine/tables.rs), host copies ---- */

@@ -2,6 +2,7 @@
 // src/engine/tables.rs (exp/log :184-221, log_walsh :223-233, skew :285-324,
 // mul :172-178); the byte-permute tables are this engine's own format.
 #include "gf_tables.hpp"
+#include "rs_device.hpp"
 
 #include <mutex>
 
@@ -121,6 +122,12 @@ GfTables *build() {
 }
 
 }  // namespace
+
+// rs_device.hpp: name of the last kernel launched by this thread (profiler records)
+char *launch_name_buf() {
+    static thread_local char name[kLaunchNameBytes];
+    return name;
+}
 
 uint16_t add_mod(uint16_t a, uint16_t b) {
     const uint32_t s = uint32_t(a) + b;

@@ -168,6 +168,7 @@ struct rs_context {
     uint16_t *d_lwfold = nullptr;
     uint16_t lw0 = 0;
     bool mono = true;             // RS_MI355X_NO_MONO=1 disables the column kernel
+    bool split = true;            // RS_MI355X_NO_SPLIT=1 disables the split decode plan (A/B)
     bool mono_all = false;        // RS_MI355X_MONO_ALL=1: unstaged column kernel too (see use_mono)
     uint32_t mono_max_packs = 256;   // column kernel only up to this many packs (RS_MI355X_MONO_MAX_PACKS)
     std::mutex img_mu;            // guards d_img
@@ -655,6 +656,16 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
             Mo.erased[r >> 5] |= uint32_t(st[r] == 1) << (r & 31);
             Mo.received[r >> 5] |= uint32_t(st[r] == 2) << (r & 31);
         }
+        if (ctx->split && rs::mono_split(int(u))) {
+            // split plan: every restored row in one half of the work rows
+            bool lower = false, upper = false;
+            for (uint32_t r = out_map.row_begin; r < out_map.row_end; ++r)
+                if (st[r] == 1) (r < nd / 2 ? lower : upper) = true;
+            if (!(lower && upper)) {
+                Mo.split = 1;
+                Mo.out_half = upper ? 1 : 0;
+            }
+        }
         launch_mono(rs::kMonoDecode, u, Mo, s, (received + missing) * uint64_t(g.packs) * 8 * g.stripes);
         return;
     }
@@ -939,6 +950,8 @@ rs_status rs_context_create(int device, rs_context **out) {
             const unsigned long k = strtoul(mk, nullptr, 10);
             if (k >= 4 && k <= kMaxK) g_max_k = uint32_t(k);
         }
+        const char *ns = getenv("RS_MI355X_NO_SPLIT");
+        ctx->split = !(ns && ns[0] == '1');
         const char *ma = getenv("RS_MI355X_MONO_ALL");
         ctx->mono_all = ma && ma[0] == '1';
         if (const char *mp = getenv("RS_MI355X_MONO_MAX_PACKS")) ctx->mono_max_packs = uint32_t(strtoul(mp, nullptr, 10));
@@ -1677,8 +1690,9 @@ rs_status rs_profile_enable(rs_context *ctx, int enable) {
 rs_status rs_mono_enable(rs_context *ctx, int enable) {
     if (!ctx) return RS_ERR_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> lock(ctx->mu);
-    ctx->mono = enable != 0;
-    ctx->mono_all = enable == 2;
+    ctx->mono = (enable & 3) != 0;
+    ctx->mono_all = (enable & 3) == 2;
+    ctx->split = !(enable & 4);
     return RS_OK;
 }
 

@@ -110,6 +110,8 @@ struct MonoArgs {
     // evaluates it; no rowinfo): erased / received bits of the 2^L work rows,
     // as in EvalArgs
     uint32_t fused_eval = 0, low_rate = 0, end = 0, lw0 = 0;
+    // split plan (mono_split(L)): every restored row lies in half out_half of the 2^L work rows
+    uint32_t split = 0, out_half = 0;
     const uint16_t *lw_fold = nullptr;
     uint32_t erased[kMonoFusedRows / 32] = {}, received[kMonoFusedRows / 32] = {};
     // a batch of stripes of one shape in one launch (staged kernel, grid.y =
@@ -124,6 +126,10 @@ hipError_t launch_mono(int mode, int L, const MonoArgs &A, hipStream_t stream);
 // Variant launch_mono picks: LDS-staged twiddles (single chunk, 2 rows per
 // lane, L <= 11); fused_eval and stripes > 1 require it.
 bool mono_staged(int L, uint32_t chunks);
+// Decodes of 2^L work rows (L in 9..11) whose restored rows all lie in one half
+// may use the split plan (MonoArgs::split): the FFT below the top layer runs
+// only on that half.
+bool mono_split(int L);
 int mono_rows_log2_per_lane(int L, uint32_t chunks);
 
 // eval_poly for a decode (src/engine/utils.rs:20-31) reduced to 2^u points

@@ -800,11 +800,6 @@ __global__ void k_formal_derivative(const uint8_t *in, uint8_t *out, uint32_t ro
 
 }  // namespace
 
-char *launch_name_buf() {
-    static thread_local char name[kLaunchNameBytes];
-    return name;
-}
-
 hipError_t launch_pass(int K, int flags, const PassArgs &A, hipStream_t s) {
     // narrow slices when the wide shape's slices leave the chip under-filled
     const uint32_t wide_packs = K >= 8 ? 16 : K == 7 ? 32 : 64;

@@ -132,15 +132,23 @@ constexpr Map seg_map(int L, int LR, int lo, const int *order, int no) {
     return m;
 }
 
-template <int L, int LR>
+// SPLIT (decodes whose restored rows lie in one half of the 2^L work rows):
+// the top row bit L-1 stays a wave bit throughout, so each half is a 2^(L-1)
+// row transform of its own waves; the IFFT stops below layer L-1, the top
+// layers of both transforms and the formal derivative's cross-half term run
+// in one exchange (split_top), and only the half holding restored rows runs
+// the rest of the FFT.
+template <int L, int LR, bool SPLIT = false>
 struct Plan {
-    static constexpr int IW = LR + 6, WB = L - IW, R = 1 << LR;
-    static_assert(WB >= 0 && WB <= 4, "column kernel: 6 lane bits + LR register bits + up to 4 wave bits");
+    static constexpr int IW = LR + 6, WB = L - IW - (SPLIT ? 1 : 0), R = 1 << LR;
+    static_assert(WB >= 0 && L - IW <= 4, "column kernel: 6 lane bits + LR register bits + up to 4 wave bits");
+    static_assert(!SPLIT || WB >= 1, "split plan: at least one wave bit below the top bit");
+    static constexpr int TOP = SPLIT ? L - 1 : L;  // layers [0, TOP) run in the sequences
 
     static constexpr Seq make_ifft() {
         Seq s{};
         int bits[16] = {}, order[32] = {}, no = 0;
-        if (WB == 0) {
+        if (WB == 0 && !SPLIT) {
             for (int x = 0; x < L; ++x) order[no++] = x;
             for (int x = L - 1; x >= 0; --x) order[no++] = x;
             Map m = seg_map(L, LR, 0, order, no);
@@ -154,14 +162,15 @@ struct Plan {
         Map m = seg_map(L, LR, 0, order, no);
         s.maps[0] = m;
         layers(s, m, LR, bits, IW);
-        // segment B: the top IW bits in-wave: IFFT layers IW..L-1 (then FFT L-1..WB)
+        // segment B: the top IW bits (below bit L-1 when SPLIT) in-wave: IFFT
+        // layers IW..TOP-1 (then FFT TOP-1..WB)
         no = 0;
-        for (int x = IW; x < L; ++x) order[no++] = x;
-        for (int x = L - 1; x >= WB; --x) order[no++] = x;
+        for (int x = IW; x < TOP; ++x) order[no++] = x;
+        for (int x = TOP - 1; x >= WB; --x) order[no++] = x;
         m = seg_map(L, LR, WB, order, no);
         push(s, Op{kOpRemap, -1, 0, 0}, m);
-        for (int x = IW; x < L; ++x) bits[x - IW] = x;
-        layers(s, m, LR, bits, L - IW);
+        for (int x = IW; x < TOP; ++x) bits[x - IW] = x;
+        layers(s, m, LR, bits, TOP - IW);
         return s;
     }
     static constexpr Seq ifft = make_ifft();
@@ -171,9 +180,9 @@ struct Plan {
         int bits[16] = {}, order[16] = {}, no = 0;
         Map m = ifft.maps[ifft.count];
         s.maps[0] = m;
-        const int stop = WB;  // FFT layers L-1..stop in the IFFT's final placement
-        for (int x = L - 1; x >= stop; --x) bits[L - 1 - x] = x;
-        layers(s, m, LR, bits, L - stop);
+        const int stop = WB;  // FFT layers TOP-1..stop in the IFFT's final placement
+        for (int x = TOP - 1; x >= stop; --x) bits[TOP - 1 - x] = x;
+        layers(s, m, LR, bits, TOP - stop);
         if (WB == 0) return s;
         // segment C: the low IW bits in-wave again, FFT layers WB-1..0
         for (int x = WB - 1; x >= 0; --x) order[no++] = x;
@@ -186,9 +195,9 @@ struct Plan {
     static constexpr Seq fft = make_fft();
 };
 
-template <int L, int LR, bool FFT>
+template <int L, int LR, bool FFT, bool SPLIT = false>
 struct SeqOf {
-    static constexpr const Seq &v = FFT ? Plan<L, LR>::fft : Plan<L, LR>::ifft;
+    static constexpr const Seq &v = FFT ? Plan<L, LR, SPLIT>::fft : Plan<L, LR, SPLIT>::ifft;
 };
 
 constexpr int layer_ordinal(const Seq &s, int i) {
@@ -311,20 +320,24 @@ struct GlobalTabs {
     }
 };
 
-template <int L, int LR>
+template <int L, int LR, bool SPLIT = false>
 struct Stage {
-    static constexpr int IW = LR + 6, WB = L - IW;
+    static constexpr int IW = LR + 6, WB = L - IW - (SPLIT ? 1 : 0);
     static constexpr uint32_t n = 1u << L, W = 1u << IW;
     // layers of the last (FFT) in-wave phase
     static constexpr int NB3 = WB > 0 ? WB : L;
-    // B0 = 1: layer 0 of phases 1 and 3 (one table per butterfly) is read from
-    // the global image instead, so the private regions fit LDS at L = 11
+    // B0 = 1: layer 0 of phases 1 and 3 (one table per butterfly) takes turns
+    // with the other layers in the private regions, so they fit LDS at L = 11
 #ifndef RS_MONO_B0_MIN_L
 #define RS_MONO_B0_MIN_L 11
 #endif
     static constexpr int B0 = L >= RS_MONO_B0_MIN_L ? 1 : 0;
-    static constexpr uint32_t kPriv = (W >> B0) - 1;                 // tables per wave region
-    static constexpr uint32_t kP3 = (W >> B0) - (W >> NB3);          // tables of phase 3
+    // tables per wave region; with B0 the region first holds layer 0's W/2
+    // tables, then (written over them, see run_seq's hook) the layers above
+    static constexpr uint32_t kPriv = B0 ? (W >> 1) : W - 1;
+    static constexpr uint32_t kUp = (W >> B0) - 1;                   // tables of phase 1 (layer 0 apart)
+    static constexpr uint32_t kP3 = (W >> B0) - (W >> NB3);          // tables of phase 3 (layer 0 apart)
+    static constexpr uint32_t kL0 = W >> 1;                          // layer-0 tables of a wave region
     static constexpr uint32_t kShI = WB > 0 ? (n >> IW) - 1 : 0;     // shared: IFFT layers IW..L-1
     static constexpr uint32_t kShF = WB > 0 ? (n >> WB) - 1 : 0;     // shared: FFT layers WB..L-1
     static constexpr uint32_t kShared = kShI + kShF;
@@ -332,6 +345,8 @@ struct Stage {
     static constexpr uint32_t plane_words = 2 * n;
     static constexpr uint32_t words = plane_words + (kShared + kWaves * kPriv) * 20;
     static constexpr uint32_t words_dec = words + n;  // + per-row decode info (fused eval_poly)
+    // SPLIT decode: + a second column plane (the cross-half step's formal-derivative values)
+    static constexpr uint32_t words_split = words_dec + (SPLIT ? plane_words : 0);
 };
 
 // Table source: tables staged in LDS (STAGED column kernel).  Phase 1 (IFFT
@@ -339,17 +354,17 @@ struct Stage {
 // wave-private region: a wave's rows there are 2^IW consecutive rows, so its
 // groups are its own.  Phase 2 (top bits in-wave, wave bits low) reads the
 // region shared by all waves.
-template <int L, int LR>
+template <int L, int LR, bool SPLIT = false>
 struct LdsTabs {
-    using G = Stage<L, LR>;
+    using G = Stage<L, LR, SPLIT>;
     const uint32_t *priv, *shared, *img_i, *img_f;
     template <int, int, typename S, int I, int PH>
     __device__ __forceinline__ void get(int x, uint32_t row, uint32_t (&t)[20]) const {
         uint32_t slot;
         const uint32_t *base;
         if constexpr ((PH == 1 || PH == 3) && G::B0 == 1 && S::v.ops[I].bit == 0) {
-            load_tab(PH == 1 ? img_i : img_f, L, 0, row, t);
-            return;
+            slot = (row & (G::W - 1)) >> 1;  // layer 0's turn in the region
+            base = priv;
         } else if constexpr (PH == 1 || PH == 3) {
             slot = (G::W >> G::B0) - (G::W >> x) + ((row & (G::W - 1)) >> (x + 1));
             base = priv;
@@ -458,35 +473,42 @@ constexpr int num_layers(const Seq &s) { return layer_ordinal(s, s.count); }
 // Layers of twiddle tables in flight ahead of the layer being computed.
 constexpr int kMonoPrefetch = RS_MONO_PF;
 
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
+
 // Run one transform sequence.  The tables of layer k + B are requested right
 // after layer k, into the registers layer k just released, so table latency
 // hides behind B - 1 layers of butterflies.  Requests never cross the remap:
 // the tables beyond it may not be in place yet (staged kernel).  `pre_remap`
-// runs just before the remap.
-// KPRE >= 0: the caller has already requested the tables of layer ordinal
-// KPRE into tpre (long before use: they come from global memory).  A wave
-// with `alive` false stops after the remap (its rows there are not needed).
-template <int L, int LR, bool FFT, int B0, int KPRE = -1, typename TS, typename PreRemap>
+// runs just before the remap.  KHOOK >= 0: hook() runs right before the
+// tables of layer ordinal KHOOK are requested (the staged kernel writes a
+// wave-private table region there that the layers before it have read).  A
+// wave with `pre` false skips the ops before the remap, with `alive` false
+// the ops after it.
+template <int L, int LR, bool FFT, int B0, int KHOOK = -1, bool SPLIT = false, typename TS, typename PreRemap,
+          typename Hook = NoHook>
 __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR> &c, uint32_t *plane, uint32_t lane, uint32_t wave,
-                                        const PreRemap &pre_remap, const uint32_t (*tpre)[20] = nullptr,
-                                        bool alive = true) {
-    using S = SeqOf<L, LR, FFT>;
+                                        const PreRemap &pre_remap, bool alive = true, bool pre = true,
+                                        const Hook &hook = Hook{}) {
+    using S = SeqOf<L, LR, FFT, SPLIT>;
     constexpr int NT = (1 << LR) / 2;
     constexpr int NL = num_layers(S::v);
     constexpr int RI = remap_index(S::v);
     constexpr int NL1 = layer_ordinal(S::v, RI);  // layers before the remap
     constexpr int B = B0 < NL ? B0 : NL;
     uint32_t tb[B][NT][20];
+    auto request = [&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if constexpr (k == KHOOK) hook();
+        load_layer_tabs<L, LR, S, layer_at(S::v, k), FFT>(ts, lane, wave, tb[k % B]);
+    };
     // first tables of a segment [k0, k1) of layer ordinals
     auto prime = [&](auto k0c, auto k1c) {
         constexpr int k0 = decltype(k0c)::value, k1 = decltype(k1c)::value;
-        static_for<k0, (k0 + B < k1 ? k0 + B : k1)>([&](auto kc) {
-            constexpr int k = decltype(kc)::value;
-            if constexpr (k != KPRE)
-                load_layer_tabs<L, LR, S, layer_at(S::v, k), FFT>(ts, lane, wave, tb[k % B]);
-        });
+        static_for<k0, (k0 + B < k1 ? k0 + B : k1)>(request);
     };
-    prime(std::integral_constant<int, 0>{}, std::integral_constant<int, NL1>{});
+    if (pre) prime(std::integral_constant<int, 0>{}, std::integral_constant<int, NL1>{});
     auto step = [&](auto ic) {
         constexpr int I = decltype(ic)::value;
         constexpr Op op = S::v.ops[I];
@@ -501,24 +523,24 @@ __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR> &c, uint32_t *p
             apply_remap<L, LR, S, I>(c, plane, lane, wave);
 #endif
             RS_MSTAMP(FFT ? 9 : 4);
-            prime(std::integral_constant<int, NL1>{}, std::integral_constant<int, NL>{});
+            if (alive) prime(std::integral_constant<int, NL1>{}, std::integral_constant<int, NL>{});
         } else {
             constexpr int k = layer_ordinal(S::v, I);
 #ifndef RS_MONO_SKIP_LAYERS
-            if constexpr (k == KPRE)
-                apply_layer<L, LR, S, I, !FFT>(*reinterpret_cast<const uint32_t(*)[NT][20]>(tpre), c);
-            else
-                apply_layer<L, LR, S, I, !FFT>(tb[k % B], c);
+            apply_layer<L, LR, S, I, !FFT>(tb[k % B], c);
 #endif
             constexpr int end = k < NL1 ? NL1 : NL;
-            if constexpr (k + B < end && k + B != KPRE) {
-                load_layer_tabs<L, LR, S, layer_at(S::v, k + B), FFT>(ts, lane, wave, tb[k % B]);
+            if constexpr (k + B < end) {
+                request(std::integral_constant<int, k + B>{});
                 asm volatile("" ::: "memory");  // keep the request here, ahead of its use
             }
         }
     };
+    // pre: run the ops before the remap (a wave whose rows there are all zero
+    // skips them: IFFT layers of zero rows give zero rows); alive: after it
     if constexpr (RI < S::v.count) {
-        static_for<0, RI + 1>(step);
+        if (pre) static_for<0, RI>(step);
+        step(std::integral_constant<int, RI>{});
         if (alive) static_for<RI + 1, S::v.count>(step);
     } else {
         static_for<0, S::v.count>(step);
@@ -527,17 +549,13 @@ __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR> &c, uint32_t *p
 
 // Decode: does this wave hold, after the FFT's remap, any row of A.dst?
 // (there the wave's rows are one block of 2^IW consecutive rows)
-template <int L, int LR>
+template <int L, int LR, bool SPLIT = false>
 __device__ __forceinline__ bool wave_stores(const MonoArgs &A, uint32_t wave) {
-    using S = SeqOf<L, LR, true>;
+    using S = SeqOf<L, LR, true, SPLIT>;
     constexpr int I = S::v.count;
     const uint32_t lo = lane_rows<S, I>(0, wave), hi = lo + (1u << (LR + 6));
     return lo < A.dst.row_end && hi > A.dst.row_begin;
 }
-
-struct NoHook {
-    __device__ __forceinline__ void operator()() const {}
-};
 
 // Base pointers of this workgroup's stripe (wave-uniform, computed once).
 struct StripeBases {
@@ -571,10 +589,10 @@ __device__ __forceinline__ uint32_t paired_row(uint32_t lane, uint32_t wave, int
 // Load transform rows `chunk * n + row` (placement: start of the IFFT) as
 // paired words; finish_col completes them.  Missing rows inside the caller's
 // matrices are read and discarded by the decode's scaling.
-template <int L, int LR>
+template <int L, int LR, bool SPLIT = false>
 __device__ __forceinline__ void issue_col(const MonoArgs &A, uint32_t chunk, uint32_t pk_off, const StripeBases &sb,
-                                          uint32_t (&w)[2 << LR], uint32_t lane, uint32_t wave) {
-    using S = SeqOf<L, LR, false>;
+                                          uint32_t (&w)[2 << LR], uint32_t lane, uint32_t wave, bool live = true) {
+    using S = SeqOf<L, LR, false, SPLIT>;
     const uint32_t base = chunk * (1u << L);
     const uint32_t half = (lane & 1u) * 32u;
     static_for<0, (2 << LR)>([&](auto jc) {
@@ -586,7 +604,7 @@ __device__ __forceinline__ void issue_col(const MonoArgs &A, uint32_t chunk, uin
         p = nullptr;
         v = r * 0x9E3779B9u + half;
 #endif
-        if (p) v = *reinterpret_cast<const uint32_t *>(p + pk_off + half);
+        if (p && live) v = *reinterpret_cast<const uint32_t *>(p + pk_off + half);
         w[j] = v;
     });
 }
@@ -599,10 +617,10 @@ struct ScaleTabs {
     uint32_t t[1 << LR][20];
     uint32_t erased;  // bit i: register i's row is not received
 };
-template <int L, int LR>
+template <int L, int LR, bool SPLIT = false>
 __device__ __forceinline__ void scale_issue(const MonoArgs &A, const uint32_t *rowinfo, ScaleTabs<L, LR> &st,
                                             uint32_t lane, uint32_t wave) {
-    using S = SeqOf<L, LR, false>;
+    using S = SeqOf<L, LR, false, SPLIT>;
     const uint32_t a = lane_rows<S, 0>(lane, wave);
     st.erased = 0;
     static_for<0, (1 << LR)>([&](auto ic) {
@@ -653,11 +671,11 @@ __device__ __forceinline__ void load_col(const MonoArgs &A, uint32_t chunk, uint
 // Store transform rows `chunk * n + row` that fall in A.dst (placement: end
 // of the FFT), paired like the loads.  REVEAL (decode): only erased rows,
 // multiplied by exp(65535 - log factor) (rate_high.rs:241-245).
-template <int L, int LR, bool REVEAL>
+template <int L, int LR, bool REVEAL, bool SPLIT = false>
 __device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *rowinfo, uint32_t chunk,
                                           uint32_t pk_off, const StripeBases &sb, Col<L, LR> &c, uint32_t lane,
                                           uint32_t wave) {
-    using S = SeqOf<L, LR, true>;
+    using S = SeqOf<L, LR, true, SPLIT>;
     constexpr int I = S::v.count;
     constexpr int R = 1 << LR;
     const uint32_t base = chunk * (1u << L);
@@ -771,6 +789,125 @@ __device__ __forceinline__ void formal_derivative(Col<L, LR> &c, uint32_t *plane
         c.lo[i] = l[i];
         c.hi[i] = h[i];
     });
+}
+
+// In-wave terms of the formal derivative (register and lane bits) of the
+// values v under placement m: out = v ^ XOR over those bits b with q_b = 0 of
+// v[q | 2^b] (src/engine/utils.rs:99-104, closed form).
+template <int LR, typename S>
+__device__ __forceinline__ void fd_in_wave(const uint32_t (&vl)[1 << LR], const uint32_t (&vh)[1 << LR],
+                                           uint32_t (&l)[1 << LR], uint32_t (&h)[1 << LR], uint32_t lane) {
+    constexpr int R = 1 << LR;
+    static_for<0, R>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        l[i] = vl[i];
+        h[i] = vh[i];
+        static_for<0, LR>([&](auto sc) {
+            constexpr int sb = decltype(sc)::value;
+            if constexpr (!((i >> sb) & 1)) {
+                l[i] ^= vl[i | (1 << sb)];
+                h[i] ^= vh[i | (1 << sb)];
+            }
+        });
+    });
+    static_for<0, 6>([&](auto jc) {
+        constexpr int J = decltype(jc)::value;
+        const uint32_t keep = (lane >> J) & 1u ? 0u : ~0u;
+        static_for<0, R>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            l[i] ^= lane_xor<J>(vl[i], lane) & keep;
+            h[i] ^= lane_xor<J>(vh[i], lane) & keep;
+        });
+    });
+}
+
+// SPLIT decode, the step between the two transforms (placement: end of the
+// split IFFT; row bit L-1 = the highest wave bit, the half).  With a = lower-half and
+// b = upper-half row of a pair (q, q + n/2):
+//   IFFT layer L-1 (engine_naive.rs:96-100):  b' = b ^ a,  a' = a ^ b' * mI
+//   formal derivative (closed form): a'' = FD_half(a') ^ b',  b'' = FD_half(b')
+//   FFT layer L-1 (engine_naive.rs:64-68):    a3 = a'' ^ b'' * mF,  b3 = b'' ^ a3
+// Only the waves of the half `out_half` (the one holding restored rows) go on
+// with the FFT; they compute both halves' values of their row positions, so
+// the other half's waves only hand over their rows.  Three barriers; every
+// wave reaches them.
+template <int L, int LR>
+__device__ __forceinline__ void split_top(Col<L, LR> &c, uint32_t *plane, uint32_t *plane2, const uint32_t *tab_i,
+                                          const uint32_t *tab_f, uint32_t lane, uint32_t wave, uint32_t out_half) {
+    using S = SeqOf<L, LR, true, true>;
+    constexpr Map m = S::v.maps[0];
+    constexpr int KT = L - 1 - (LR + 6);  // the wave bit holding the top row bit (the half)
+    static_assert(m.wave[KT] == L - 1, "split placement: the top row bit is the highest wave bit");
+    constexpr uint32_t n = 1u << L, H = n >> 1;
+    constexpr int R = 1 << LR;
+    const uint32_t a = lane_rows<S, 0>(lane, wave);
+    const bool out = (wave >> KT) == out_half;
+    __syncthreads();  // the plane's previous readers are done
+    static_for<0, R>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const uint32_t x = swz<L>(a | reg_rows<S, 0, LR>(i));
+        plane[x] = c.lo[i];
+        plane[n + x] = c.hi[i];
+    });
+    __syncthreads();
+    uint32_t ll[R], lh[R], ul[R], uh[R];  // lower / upper half values of the lane's row positions
+    uint32_t fl[R], fh[R], gl[R], gh[R];  // their in-wave derivative terms
+    uint32_t tf[20];
+    if (out) {
+        uint32_t ti[20];
+        static_for<0, 5>([&](auto qc) {  // the top layers' tables: one each, wave-uniform
+            constexpr int q = decltype(qc)::value;
+            const uint4 v = reinterpret_cast<const uint4 *>(tab_i)[q];
+            ti[4 * q] = v.x, ti[4 * q + 1] = v.y, ti[4 * q + 2] = v.z, ti[4 * q + 3] = v.w;
+            const uint4 w = reinterpret_cast<const uint4 *>(tab_f)[q];
+            tf[4 * q] = w.x, tf[4 * q + 1] = w.y, tf[4 * q + 2] = w.z, tf[4 * q + 3] = w.w;
+        });
+        static_for<0, R>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            const uint32_t x = swz<L>((a | reg_rows<S, 0, LR>(i)) ^ H);
+            const uint32_t pl = plane[x], ph = plane[n + x];
+            ll[i] = out_half ? pl : c.lo[i];
+            lh[i] = out_half ? ph : c.hi[i];
+            ul[i] = out_half ? c.lo[i] : pl;
+            uh[i] = out_half ? c.hi[i] : ph;
+            ifft_bfly(ll[i], lh[i], ul[i], uh[i], ti);
+            // both halves' values, at their own rows, for the wave-bit terms
+            const uint32_t y = swz<L>((a | reg_rows<S, 0, LR>(i)) & (H - 1));
+            plane2[y] = ll[i];
+            plane2[n + y] = lh[i];
+            plane2[y + H] = ul[i];  // (the upper value of position q sits at swz(q) + H)
+            plane2[n + y + H] = uh[i];
+        });
+        fd_in_wave<LR, S>(ll, lh, fl, fh, lane);
+        fd_in_wave<LR, S>(ul, uh, gl, gh, lane);
+    }
+    __syncthreads();
+    if (out) {
+        static_for<0, KT>([&](auto kc) {  // wave bits below the top bit (wave-uniform branches)
+            constexpr int k = decltype(kc)::value;
+            if constexpr (m.wave[k] >= 0) {
+                if (!((wave >> k) & 1u)) {
+                    static_for<0, R>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value;
+                        const uint32_t q = ((a | reg_rows<S, 0, LR>(i)) & (H - 1)) ^ (1u << m.wave[k]);
+                        const uint32_t x = swz<L>(q);
+                        fl[i] ^= plane2[x];
+                        fh[i] ^= plane2[n + x];
+                        gl[i] ^= plane2[x + H];
+                        gh[i] ^= plane2[n + x + H];
+                    });
+                }
+            }
+        });
+        static_for<0, R>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            fl[i] ^= ul[i];  // bit L-1 term: lower rows take their upper partner (pre-derivative)
+            fh[i] ^= uh[i];
+            fft_bfly(fl[i], fh[i], gl[i], gh[i], tf);
+            c.lo[i] = out_half ? gl[i] : fl[i];
+            c.hi[i] = out_half ? gh[i] : fh[i];
+        });
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -892,9 +1029,9 @@ __device__ __forceinline__ void col_eval_poly(const MonoArgs &A, uint32_t ebits,
 // LDS staging of the twiddle tables (STAGED kernel): 16-byte pieces q of the
 // wave-private region (phase 1 from the IFFT image, phase 3 from the FFT
 // image) and of the shared region.
-template <int L, int LR>
+template <int L, int LR, bool SPLIT = false>
 __device__ __forceinline__ uint4 priv_piece(const uint32_t *img, uint32_t wave, uint32_t q) {
-    using G = Stage<L, LR>;
+    using G = Stage<L, LR, SPLIT>;
     const uint32_t t = q / 5, piece = q - t * 5;
     const uint32_t y = (G::W >> G::B0) - t;                   // in [1, W >> B0]
     const int b = G::IW - int(32 - __builtin_clz(y - 1));    // IW - ceil(log2 y)
@@ -902,9 +1039,16 @@ __device__ __forceinline__ uint4 priv_piece(const uint32_t *img, uint32_t wave, 
     const uint32_t slot = G::n - (G::n >> b) + wave * (G::W >> (b + 1)) + local;
     return reinterpret_cast<const uint4 *>(img)[slot * 5u + piece];
 }
-template <int L, int LR>
+// 16-byte piece q of the layer-0 tables of wave `wave`'s phase-1 / -3 rows
+// (image slots wave * W/2 .. : contiguous, one coalesced read per wave)
+template <int L, int LR, bool SPLIT = false>
+__device__ __forceinline__ uint4 l0_piece(const uint32_t *img, uint32_t wave, uint32_t q) {
+    using G = Stage<L, LR, SPLIT>;
+    return reinterpret_cast<const uint4 *>(img)[wave * G::kL0 * 5u + q];
+}
+template <int L, int LR, bool SPLIT = false>
 __device__ __forceinline__ uint4 shared_piece(const uint32_t *img_i, const uint32_t *img_f, uint32_t q) {
-    using G = Stage<L, LR>;
+    using G = Stage<L, LR, SPLIT>;
     const uint32_t t = q / 5, piece = q - t * 5;
     const uint32_t slot = t < G::kShI ? G::n - (G::n >> G::IW) + t : G::n - (G::n >> G::WB) + (t - G::kShI);
     return reinterpret_cast<const uint4 *>(t < G::kShI ? img_i : img_f)[slot * 5u + piece];
@@ -914,10 +1058,11 @@ __device__ __forceinline__ uint4 shared_piece(const uint32_t *img_i, const uint3
 #define RS_MONO_LDS_PF 2
 #endif
 
-template <int L, int LR, int MODE, bool STAGED, bool BATCH>
+template <int L, int LR, int MODE, bool STAGED, bool BATCH, bool SPLIT>
 __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
     using C = Col<L, LR>;
-    using G = Stage<L, LR>;
+    using G = Stage<L, LR, SPLIT>;
+    static_assert(!SPLIT || (STAGED && MODE == kMonoDecode), "split plan: staged decode only");
     constexpr int R = 1 << LR;
     constexpr uint32_t T = 1u << (L - LR);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -946,10 +1091,23 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
         uint32_t *shared = lds + G::plane_words;
         uint32_t *priv = shared + G::kShared * 20 + wave * G::kPriv * 20;
         uint32_t *rinfo = lds + G::words;  // decode with fused eval_poly
-        constexpr int KP1 = (5 * G::kPriv + 63) / 64;
+        constexpr int KP1 = (5 * G::kUp + 63) / 64;
+        constexpr int KP0 = G::B0 ? (5 * G::kL0 + 63) / 64 : 1;
         constexpr int KP3 = G::kP3 ? (5 * G::kP3 + 63) / 64 : 1;  // (guarded by q < 5 * kP3)
         constexpr int KSH = G::kShared ? (5 * G::kShared + T - 1) / T : 1;
         RS_MSTAMP(0);
+        // decode: does this wave's phase-1 row block (2^IW consecutive rows) hold a
+        // received row?  If not its rows are zero through phase 1: it loads no
+        // rows and no phase-1 tables, and skips the phase-1 layers
+        bool live = true;
+        if constexpr (DEC) {
+            constexpr uint32_t kWords = (1u << G::IW) / 32;
+            uint32_t any = 0;
+            static_for<0, kWords>([&](auto kc) { any |= A.received[wave * kWords + decltype(kc)::value]; });
+            live = any != 0;
+        }
+        // split decode: does this wave's half go on with the FFT (restored rows)?
+        const bool out_wave = !SPLIT || (wave >> (L - 1 - G::IW)) == A.out_half;
         // every global read is requested before any of them is waited for
         // (no branches between them: a branch would make the compiler wait)
         uint32_t ebits = 0, rbits = 0, lw[2] = {0, 0};
@@ -961,21 +1119,24 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             lw[1] = A.lw_fold[i0 + 1];
         }
         uint32_t w[2 << LR];
-        issue_col<L, LR>(A, 0, pk_off, sb, w, lane, wave);
-        // B0: layer 0's tables come from the image; request them with the rows
-        using SI = SeqOf<L, LR, false>;
-        uint32_t t0[R / 2][20];
-        if constexpr (G::B0)
-            load_layer_tabs<L, LR, SI, layer_at(SI::v, 0), false>(GlobalTabs{img_i}, lane, wave, t0);
-        uint4 v1[KP1], vs[KSH];
+        issue_col<L, LR, SPLIT>(A, 0, pk_off, sb, w, lane, wave, live);
+        // phase-1 tables (a wave that skips phase 1 reads one table: no branch
+        // around the loads); B0: layer 0's go into the region first, the
+        // layers above when layer 0 has read them (run_seq's hook)
+        uint4 v0[KP0], v1[KP1], vs[KSH];
 #ifndef RS_MONO_SKIP_STAGE  // tools/mono_probe.hip ablation
+        if constexpr (G::B0)
+            static_for<0, KP0>([&](auto kc) {
+                const uint32_t q = lane + 64u * decltype(kc)::value;
+                if (q < 5 * G::kL0) v0[kc] = l0_piece<L, LR, SPLIT>(img_i, wave, live ? q : q % 5u);
+            });
         static_for<0, KP1>([&](auto kc) {
             const uint32_t q = lane + 64u * decltype(kc)::value;
-            if (q < 5 * G::kPriv) v1[kc] = priv_piece<L, LR>(img_i, wave, q);
+            if (q < 5 * G::kUp) v1[kc] = priv_piece<L, LR, SPLIT>(img_i, wave, live ? q : q % 5u);
         });
         static_for<0, KSH>([&](auto kc) {
             const uint32_t q = threadIdx.x + T * decltype(kc)::value;
-            if (q < 5 * G::kShared) vs[kc] = shared_piece<L, LR>(img_i, img_f, q);
+            if (q < 5 * G::kShared) vs[kc] = shared_piece<L, LR, SPLIT>(img_i, img_f, q);
         });
 #endif
         const uint32_t *ri = A.rowinfo;
@@ -991,12 +1152,23 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             RS_MSTAMP(2);
         }
         ScaleTabs<L, LR> st;
-        if constexpr (DEC) scale_issue<L, LR>(A, ri, st, lane, wave);
+        if constexpr (DEC) scale_issue<L, LR, SPLIT>(A, ri, st, lane, wave);
+        auto write1 = [&]() {
 #ifndef RS_MONO_SKIP_STAGE
-        static_for<0, KP1>([&](auto kc) {
-            const uint32_t q = lane + 64u * decltype(kc)::value;
-            if (q < 5 * G::kPriv) reinterpret_cast<uint4 *>(priv)[q] = v1[kc];
-        });
+            static_for<0, KP1>([&](auto kc) {
+                const uint32_t q = lane + 64u * decltype(kc)::value;
+                if (q < 5 * G::kUp) reinterpret_cast<uint4 *>(priv)[q] = v1[kc];
+            });
+#endif
+        };
+#ifndef RS_MONO_SKIP_STAGE
+        if constexpr (G::B0)
+            static_for<0, KP0>([&](auto kc) {
+                const uint32_t q = lane + 64u * decltype(kc)::value;
+                if (q < 5 * G::kL0) reinterpret_cast<uint4 *>(priv)[q] = v0[kc];
+            });
+        else
+            write1();
         static_for<0, KSH>([&](auto kc) {
             const uint32_t q = threadIdx.x + T * decltype(kc)::value;
             if (q < 5 * G::kShared) reinterpret_cast<uint4 *>(shared)[q] = vs[kc];
@@ -1005,14 +1177,14 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
         RS_MSTAMP(6);
         finish_col<L, LR, DEC>(w, &st, c, lane);
         RS_MSTAMP(1);
-        const LdsTabs<L, LR> ts{priv, shared, img_i, img_f};
+        const LdsTabs<L, LR, SPLIT> ts{priv, shared, img_i, img_f};
         // phase-3 tables: requested when phase 1 ends, written over this wave's
         // phase-1 tables when phase 2 ends
         uint4 v3[KP3];
         auto issue3 = [&]() {
             static_for<0, KP3>([&](auto kc) {
                 const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < 5 * G::kP3) v3[kc] = priv_piece<L, LR>(img_f, wave, q);
+                if (q < 5 * G::kP3) v3[kc] = priv_piece<L, LR, SPLIT>(img_f, wave, out_wave ? q : q % 5u);
             });
         };
         auto write3 = [&]() {
@@ -1021,22 +1193,59 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
                 if (q < 5 * G::kP3) reinterpret_cast<uint4 *>(priv)[q] = v3[kc];
             });
         };
-        if constexpr (G::WB > 0) {
-            run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 0 : -1>(ts, c, plane, lane, wave, issue3, t0);
+        // B0: the FFT's layer-0 tables (phase 3's last layer), requested while the
+        // FFT's phase 2 runs, take their turn in the region before that layer
+        uint4 v4[KP0];
+        auto issue4 = [&](bool need) {
+            if constexpr (G::B0)
+                static_for<0, KP0>([&](auto kc) {
+                    const uint32_t q = lane + 64u * decltype(kc)::value;
+                    if (q < 5 * G::kL0) v4[kc] = l0_piece<L, LR, SPLIT>(img_f, wave, need ? q : q % 5u);
+                });
+        };
+        auto write4 = [&]() {
+            if constexpr (G::B0)
+                static_for<0, KP0>([&](auto kc) {
+                    const uint32_t q = lane + 64u * decltype(kc)::value;
+                    if (q < 5 * G::kL0) reinterpret_cast<uint4 *>(priv)[q] = v4[kc];
+                });
+        };
+        if constexpr (SPLIT) {
+            // the wave's half: the highest wave bit in both placements
+            constexpr uint32_t kHalfWords = (G::n / 2) / 32;
+            uint32_t half_any = 0;
+            const uint32_t h = wave >> (L - 1 - G::IW);
+            for (uint32_t k = 0; k < kHalfWords; ++k) half_any |= A.received[h * kHalfWords + k];
+            // IFFT: a wave whose rows hold no received row skips phase 1 (its rows
+            // stay zero), a half without received rows skips phase 2
+            run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 1 : -1, true>(ts, c, plane, lane, wave, issue3,
+                                                                         half_any != 0, live, write1);
+            using SF = SeqOf<L, LR, true, true>;
+            constexpr int NLF = num_layers(SF::v);
+            const bool out = out_wave;
+            const bool alive = out && wave_stores<L, LR, true>(A, wave);
+            constexpr uint32_t kTopI = (G::n >> G::IW) - 2, kTopF = G::kShI + (G::n >> G::WB) - 2;
+            split_top<L, LR>(c, plane, lds + G::words_dec, shared + kTopI * 20, shared + kTopF * 20, lane, wave,
+                             A.out_half);
+            issue4(alive);
+            // FFT below the top layer: only the half that holds restored rows
+            run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, true>(ts, c, plane, lane, wave, write3, alive,
+                                                                              out, write4);
+            if (!alive) return;
+        } else if constexpr (G::WB > 0) {
+            run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 1 : -1>(ts, c, plane, lane, wave, issue3, true, live,
+                                                                   write1);
             RS_MSTAMP(5);
-            // B0: the FFT's last layer (row bit 0) reads the image too; request
-            // its tables now, a whole FFT phase ahead of their use
             using SF = SeqOf<L, LR, true>;
             constexpr int NLF = num_layers(SF::v);
-            uint32_t tl[R / 2][20];
             const bool alive = !DEC || wave_stores<L, LR>(A, wave);
-            if constexpr (G::B0)  // (waves that stop early all read one table: no branch around the loads)
-                load_layer_tabs<L, LR, SF, layer_at(SF::v, NLF - 1), true>(GlobalTabs{img_f}, alive ? lane : 0u, wave,
-                                                                             tl);
+            issue4(alive);  // (waves that stop early all read one table: no branch around the loads)
             if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
-            run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1>(ts, c, plane, lane, wave, write3, tl, alive);
+            run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1>(ts, c, plane, lane, wave, write3, alive, true,
+                                                                        write4);
             if (!alive) return;
         } else {
+            static_assert(!G::B0, "one-segment plans keep every table in the region");
             run_seq<L, LR, false, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, NoHook{});
             issue3();
             if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
@@ -1044,7 +1253,7 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             run_seq<L, LR, true, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, NoHook{});
         }
         RS_MSTAMP(10);
-        store_col<L, LR, DEC>(A, ri, 0, pk_off, sb, c, lane, wave);
+        store_col<L, LR, DEC, SPLIT>(A, ri, 0, pk_off, sb, c, lane, wave);
         RS_MSTAMP(11);
     } else if constexpr (MODE == kMonoEncodeHigh) {
         // rate_high.rs:44-87: recovery = FFT_0(XOR_c IFFT_{c n + n}(chunk c))
@@ -1093,26 +1302,29 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
 // log2 rows per lane (2^(L - LR) threads, at most 1024): the staged variant
 // keeps 2 rows per lane (L <= 11); the unstaged one at most 512 threads
 constexpr bool staged_l(int L) { return L <= RS_MONO_STAGED_MAX_L && (L >= 11 || RS_MONO_LR10 == 1); }
+// the split decode plan needs a wave bit below the top bit: 2^(LR + 6 + 2) rows or more
+constexpr bool split_l(int L) { return L >= 9 && L <= 11; }
 constexpr int mono_lr(int L, bool staged) {
     return staged ? 1 : L <= 10 ? (RS_MONO_LR10 < L - 6 ? RS_MONO_LR10 : L - 6) : L - 9;
 }
 
-template <int L, int MODE, bool STAGED, bool BATCH = false>
+template <int L, int MODE, bool STAGED, bool BATCH = false, bool SPLIT = false>
 hipError_t launch_ls(const MonoArgs &A, hipStream_t s) {
     constexpr int LR = mono_lr(L, STAGED);
-    const size_t lds = STAGED ? size_t(MODE == kMonoDecode ? Stage<L, LR>::words_dec : Stage<L, LR>::words) * 4
+    using G = Stage<L, LR, SPLIT>;
+    const size_t lds = STAGED ? size_t(SPLIT ? G::words_split : MODE == kMonoDecode ? G::words_dec : G::words) * 4
                               : size_t(8) << L;
     static bool attr_set = false;  // benign race: idempotent attribute call
     if (!attr_set && lds > 65536) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mono<L, LR, MODE, STAGED, BATCH>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mono<L, LR, MODE, STAGED, BATCH, SPLIT>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const uint32_t grid = 8u * A.packs_per_xcd;
-    k_mono<L, LR, MODE, STAGED, BATCH><<<dim3(grid, BATCH ? A.stripes : 1), 1 << (L - LR), lds, s>>>(A);
-    snprintf(launch_name_buf(), kLaunchNameBytes, "k_mono<%d, %d, %d, %s, %s>", L, LR, MODE, STAGED ? "true" : "false",
-             BATCH ? "true" : "false");
+    k_mono<L, LR, MODE, STAGED, BATCH, SPLIT><<<dim3(grid, BATCH ? A.stripes : 1), 1 << (L - LR), lds, s>>>(A);
+    snprintf(launch_name_buf(), kLaunchNameBytes, "k_mono<%d, %d, %d, %s, %s, %s>", L, LR, MODE,
+             STAGED ? "true" : "false", BATCH ? "true" : "false", SPLIT ? "true" : "false");
     return hipGetLastError();
 }
 
@@ -1123,6 +1335,12 @@ hipError_t launch_l(const MonoArgs &A, hipStream_t s) {
     if constexpr (staged_l(L)) {
         if (A.chunks == 1) {  // = mono_staged()
             if (MODE == kMonoDecode && !A.fused_eval) return hipErrorInvalidValue;
+            if constexpr (MODE == kMonoDecode && split_l(L)) {
+                if (A.split) {
+                    if (A.stripes > 1) return launch_ls<L, MODE, true, true, true>(A, s);
+                    return launch_ls<L, MODE, true, false, true>(A, s);
+                }
+            }
             if (A.stripes > 1) return launch_ls<L, MODE, true, true>(A, s);
             return launch_ls<L, MODE, true>(A, s);
         }
@@ -1147,6 +1365,7 @@ hipError_t launch_m(int L, const MonoArgs &A, hipStream_t s) {
 }  // namespace
 
 bool mono_staged(int L, uint32_t chunks) { return L >= 7 && staged_l(L) && chunks == 1; }
+bool mono_split(int L) { return split_l(L) && staged_l(L); }
 int mono_rows_log2_per_lane(int L, uint32_t chunks) { return mono_lr(L, mono_staged(L, chunks)); }
 
 hipError_t launch_mono(int mode, int L, const MonoArgs &A, hipStream_t s) {

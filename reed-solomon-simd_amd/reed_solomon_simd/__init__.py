@@ -641,6 +641,13 @@ def _check_matrix(x, rows: int, shard_bytes: int, what: str, dims: int = 2, on_d
         raise ValueError(f"{what}: shape {tuple(x.shape)} does not hold {rows} rows of {shard_bytes} bytes")
 
 
+def _validate(rate_: int, original_count: int, recovery_count: int, shard_bytes: int) -> None:
+    """The reference's own checks first (UnsupportedShardCount, then InvalidShardSize:
+    src/rate.rs:91-106), so argument-shape errors never mask them."""
+    err = _RsError()
+    _raise(_lib.rs_validate(rate_, original_count, recovery_count, shard_bytes, ctypes.byref(err)), err)
+
+
 def _check_mask(mask: bytes, count: int, what: str) -> bytes:
     if len(mask) != count:
         raise ValueError(f"{what}: {len(mask)} flags for {count} shards")
@@ -654,6 +661,7 @@ def encode_device(original_count: int, recovery_count: int, shard_bytes: int, d_
     d_original / d_recovery: torch uint8 tensors [count, shard_bytes] (column-slice views of wider
     matrices allowed) or raw device pointers to contiguous rows."""
     ctx = ctx or default_context()
+    _validate(rate_, original_count, recovery_count, shard_bytes)
     _check_matrix(d_original, original_count, shard_bytes, "d_original")
     _check_matrix(d_recovery, recovery_count, shard_bytes, "d_recovery")
     err = _RsError()
@@ -675,6 +683,7 @@ def encode_device_batch(original_count: int, recovery_count: int, shard_bytes: i
     """Encode a batch of stripes of one shape (rs_encode_device_batch): d_original
     [stripes, original_count, shard_bytes], d_recovery [stripes, recovery_count, shard_bytes]."""
     ctx = ctx or default_context()
+    _validate(rate_, original_count, recovery_count, shard_bytes)
     _check_matrix(d_original, original_count, shard_bytes, "d_original", 3)
     _check_matrix(d_recovery, recovery_count, shard_bytes, "d_recovery", 3)
     if d_original.shape[0] != d_recovery.shape[0]:
@@ -692,6 +701,7 @@ def decode_device_batch(original_count: int, recovery_count: int, shard_bytes: i
     """Decode a batch of stripes sharing ONE erasure pattern (rs_decode_device_batch); tensors
     [stripes, rows, shard_bytes]; only missing originals of d_restored are written."""
     ctx = ctx or default_context()
+    _validate(rate_, original_count, recovery_count, shard_bytes)
     _check_matrix(d_original, original_count, shard_bytes, "d_original", 3)
     _check_matrix(d_recovery, recovery_count, shard_bytes, "d_recovery", 3)
     _check_matrix(d_restored, original_count, shard_bytes, "d_restored", 3)
@@ -722,6 +732,7 @@ def decode_device(original_count: int, recovery_count: int, shard_bytes: int, d_
                   d_recovery, recovery_present, d_restored, stream=None, rate_: int = RATE_DEFAULT,
                   ctx: Optional[Context] = None) -> None:
     ctx = ctx or default_context()
+    _validate(rate_, original_count, recovery_count, shard_bytes)
     op = _check_mask(present_mask(original_present), original_count, "original_present")
     rp = _check_mask(present_mask(recovery_present), recovery_count, "recovery_present")
     _check_matrix(d_original, original_count, shard_bytes, "d_original")
@@ -759,6 +770,7 @@ def encode_device_call(original_count: int, recovery_count: int, shard_bytes: in
                        stream=None, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None) -> DeviceCall:
     """encode_device(...) bound once; call the result to encode."""
     ctx = ctx or default_context()
+    _validate(rate_, original_count, recovery_count, shard_bytes)
     _check_matrix(d_original, original_count, shard_bytes, "d_original")
     _check_matrix(d_recovery, recovery_count, shard_bytes, "d_recovery")
     u = ctypes.c_uint64
@@ -773,6 +785,7 @@ def decode_device_call(original_count: int, recovery_count: int, shard_bytes: in
                        ctx: Optional[Context] = None) -> DeviceCall:
     """decode_device(...) bound once; call the result to decode."""
     ctx = ctx or default_context()
+    _validate(rate_, original_count, recovery_count, shard_bytes)
     op = _check_mask(present_mask(original_present), original_count, "original_present")
     rp = _check_mask(present_mask(recovery_present), recovery_count, "recovery_present")
     _check_matrix(d_original, original_count, shard_bytes, "d_original")

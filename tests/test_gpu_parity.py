@@ -846,6 +846,47 @@ def test_decode_loss_patterns_pruned_reveal(torch, rs, kind, rate, N, M, S, mono
         rs.mono_enable(1)
 
 
+SPLIT_CASES = [
+    # (rate, N, M, S): 2^9 .. 2^11 work rows, restored rows in the upper (high) / lower (low) half
+    ("high", 1024, 1024, 1024), ("low", 1024, 1000, 512), ("high", 512, 512, 640), ("low", 512, 300, 192),
+    ("high", 256, 256, 128), ("low", 256, 200, 64), ("high", 700, 1000, 256), ("high", 1500, 500, 192),
+]
+
+
+@pytest.mark.parametrize("kind", ["tail", "head", "one", "random", "all", "straddle"])
+@pytest.mark.parametrize("rate,N,M,S", SPLIT_CASES)
+def test_split_decode_matches_oracle(torch, rs, rate, N, M, S, kind):
+    """Column-kernel decodes under the split plan (restored rows in one half of the work rows:
+    only that half runs the FFT below the top layer) and, for losses in both halves of
+    1500:500 (work rows 512..2011 hold originals), the unsplit plan; split on and off give
+    the same bytes."""
+    orig = O.generate_original(N, S, 17)
+    rec = O.encode(rate, orig, M)
+    rng = np.random.default_rng(N + M + S)
+    if kind == "straddle":
+        op = np.ones(N, np.uint8)
+        op[[0, N // 2, N - 1]] = 0
+    else:
+        op = _loss_pattern(kind, N, rng)
+    L = int((op == 0).sum())
+    if L > M:
+        pytest.skip("more losses than recovery shards")
+    rp = np.zeros(M, np.uint8)
+    rp[rng.choice(M, L, replace=False)] = 1
+    outs = []
+    for flag in (1, 1 | 4):
+        rs.mono_enable(flag)
+        try:
+            outs.append(gpu_decode(torch, rs, rate, orig, op, rec, rp))
+        finally:
+            rs.mono_enable(1)
+    miss = op == 0
+    for got in outs:
+        assert np.array_equal(got[miss], orig[miss])
+        assert np.all(got[~miss] == 0x33), "present rows of the output must not be written"
+    rs.check_device()
+
+
 def test_bound_device_calls_match_oracle(torch, rs):
     """encode_device_call / decode_device_call (the bench's timed calls) = the oracle."""
     N, M, S = 1024, 1024, 1024

@@ -8,6 +8,7 @@
 #include "../reed-solomon-simd_amd/csrc/rs_mono.hip"
 
 #include <algorithm>
+#include <string>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -86,6 +87,8 @@ int main(int argc, char **argv) {
         A.lut = d_lut;
         // "d1": the 1 % pattern (recovery 0..11 and originals 0..n/2-12 received)
         const bool one = argv[3][1] == '1';
+        // "...s": the split plan (restored rows = the upper half's erased originals)
+        if (std::string(argv[3]).find('s') != std::string::npos) A.split = 1, A.out_half = 1;
         for (uint32_t r = 0; r < n; ++r) {
             const bool rcv = one ? (r < 12 || (r >= n / 2 && r < n - 11)) : r < n / 2;
             if (rcv) A.received[r >> 5] |= 1u << (r & 31);
@@ -104,7 +107,8 @@ int main(int argc, char **argv) {
     CK(hipEventSynchronize(b));
     float ms;
     CK(hipEventElapsedTime(&ms, a, b));
-    printf("mono %s n=%u S=%u: %.2f us/launch (back-to-back)\n", dec ? "decode" : "encode", n, S, ms * 1000 / iters);
+    printf("mono %s%s n=%u S=%u: %.2f us/launch (back-to-back)\n", dec ? "decode" : "encode", A.split ? " split" : "", n,
+           S, ms * 1000 / iters);
     {  // floor: an empty kernel with the same grid, block and LDS
         const size_t lds = size_t(rs::Stage<10, 1>::words_dec) * 4;
         CK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_empty_lds), hipFuncAttributeMaxDynamicSharedMemorySize,
