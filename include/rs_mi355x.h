@@ -152,9 +152,11 @@ void rs_decoder_free(rs_decoder *dec);
 
 /* ---- device-resident batch path (HBM in, HBM out) ----
  * d_original: original_count rows, d_recovery: recovery_count rows, both
- * row-major with row stride shard_bytes.  shard_bytes must be a positive
- * multiple of 64 (the reference's native block layout, algorithm.md:18-31;
- * other even sizes go through the host API, which re-packs the tail block).
+ * row-major with row stride shard_bytes.  shard_bytes: any positive even
+ * size (Error::InvalidShardSize otherwise); whole 64-byte blocks use the
+ * reference's block layout (algorithm.md:18-31) and the last S % 64 bytes its
+ * tail layout (S % 64 / 2 low bytes, then the high bytes: src/engine/shards.rs:38-74),
+ * so shards are byte-identical to the reference's Encoder / Decoder output.
  * Asynchronous on `stream` (device scratch per context and stream: see
  * "Thread-safety" above). */
 rs_status rs_encode_device(rs_context *ctx, rs_rate rate, uint64_t original_count, uint64_t recovery_count,
@@ -168,8 +170,9 @@ rs_status rs_decode_device(rs_context *ctx, rs_rate rate, uint64_t original_coun
                            const void *d_recovery, const uint8_t *recovery_present, void *d_restored, void *stream,
                            rs_error *err);
 /* Column slices of wider matrices: shard r of a matrix starts at base + r * stride
- * (stride 0 = shard_bytes; otherwise >= shard_bytes and a multiple of 4; device
- * pointers 4-byte aligned).  Every engine op is column-wise
+ * (stride 0 = shard_bytes; otherwise >= shard_bytes).  Any alignment works:
+ * when a base address or stride is not a multiple of 4 the kernels access the
+ * caller's matrices byte by byte (slower).  Every engine op is column-wise
  * (src/engine/utils.rs:35-43), so encoding a range of whole 64-byte blocks of
  * each shard yields exactly those blocks of the full recovery shards: the
  * building block of the column-partitioned multi-GPU encode. */
@@ -210,7 +213,8 @@ rs_status rs_decode_device_batch(rs_context *ctx, rs_rate rate, uint64_t origina
  * the runtime.  The byte axis is cut into `slices` column slices of whole
  * 64-byte blocks (0 = 1); slice k is copied in, coded and copied out on its
  * own stream, overlapping neighbouring slices.  Blocking: returns when the
- * outputs are in host memory.  shard_bytes must be a multiple of 64.
+ * outputs are in host memory.  shard_bytes: any even size (the tail block
+ * travels with the last slice).
  * Decode copies in only received rows and writes only the missing originals
  * of h_restored (original_count x shard_bytes). */
 void *rs_host_alloc(uint64_t bytes);

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <initializer_list>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -247,10 +248,35 @@ struct Geom {
     // bytes after the base pointers (rs_encode_device_batch / rs_decode_device_batch)
     uint32_t stripes = 1;
     uint64_t orig_bstride = 0, rec_bstride = 0, out_bstride = 0;
+    rs::ShardFormat fmt;  // byte layout of the caller's matrices (tails, alignment)
     uint64_t orig() const { return orig_stride ? orig_stride : stride; }
     uint64_t rec() const { return rec_stride ? rec_stride : stride; }
     uint64_t out() const { return out_stride ? out_stride : stride; }
 };
+
+// Packs of a shard of S bytes: 8 per whole 64-byte block, then one per 4
+// elements of the tail block (S % 64 bytes = (S % 64) / 2 elements).
+uint32_t packs_of(uint64_t S) { return uint32_t(S / 64 * 8 + ((S % 64) / 2 + 3) / 4); }
+
+// Geometry of a device call on the caller's matrices of shards of S bytes
+// (any even S: the tail block follows the reference's layout,
+// src/engine/shards.rs:38-74; rs_device.hpp ShardFormat).  Strides 0 = S.
+// Work buffers use rows of whole 64-byte blocks.
+Geom device_geom(uint64_t S, uint64_t orig_stride, uint64_t rec_stride, uint64_t out_stride,
+                 std::initializer_list<const void *> ptrs) {
+    Geom g{round_up(S, 64), packs_of(S)};
+    g.orig_stride = orig_stride ? orig_stride : S;
+    g.rec_stride = rec_stride ? rec_stride : S;
+    g.out_stride = out_stride ? out_stride : S;
+    bool aligned = g.orig_stride % 4 == 0 && g.rec_stride % 4 == 0 && g.out_stride % 4 == 0;
+    for (const void *p : ptrs) aligned = aligned && (reinterpret_cast<uintptr_t>(p) & 3) == 0;
+    if (S % 64 || !aligned) {
+        g.fmt.full_packs = uint32_t(S / 64 * 8);
+        g.fmt.tail_h = uint32_t(S % 64 / 2);
+        g.fmt.io_bytes = aligned ? 0 : 1;
+    }
+    return g;
+}
 
 rs::PassArgs base_args(rs_context *ctx, const Geom &g, uint32_t n) {
     rs::PassArgs A;
@@ -259,6 +285,7 @@ rs::PassArgs base_args(rs_context *ctx, const Geom &g, uint32_t n) {
     A.slices = (g.packs + 63) / 64;
     A.tw = ctx->d_tw;
     A.lut = ctx->d_lut;
+    A.fmt = g.fmt;
     return A;
 }
 
@@ -375,6 +402,7 @@ rs::MonoArgs mono_args(rs_context *ctx, uint32_t L, const Geom &g) {
     M.img = mono_images(ctx, L);
     M.img_words = uint64_t((1u << L) - 1) * rs::kPermWords;
     M.lut = ctx->d_lut;
+    M.fmt = g.fmt;
     return M;
 }
 
@@ -1008,8 +1036,10 @@ uint64_t rs_decoder_work_count(rs_rate rate, uint64_t N, uint64_t M) {
 // ---- device-resident ------------------------------------------------------
 
 namespace {
-bool stride_ok(uint64_t stride, uint64_t S) { return stride == 0 || (stride >= S && stride % 4 == 0); }
-bool ptr_ok(const void *p) { return p && (reinterpret_cast<uintptr_t>(p) & 3) == 0; }
+// any row stride that holds a shard (0 = shard_bytes); any device address:
+// unaligned matrices go byte by byte (ShardFormat::io_bytes)
+bool stride_ok(uint64_t stride, uint64_t S) { return stride == 0 || stride >= S; }
+bool ptr_ok(const void *p) { return p != nullptr; }
 }  // namespace
 
 rs_status rs_encode_device_strided(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S,
@@ -1018,14 +1048,12 @@ rs_status rs_encode_device_strided(rs_context *ctx, rs_rate rate, uint64_t N, ui
     if (!ctx || !ptr_ok(d_orig) || !ptr_ok(d_rec)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     const int high = resolve(rate, N, M, S, err);
     if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
-    if (S % 64 || !stride_ok(orig_stride, S) || !stride_ok(rec_stride, S)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    if (!stride_ok(orig_stride, S) || !stride_ok(rec_stride, S)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     return guarded(err, [&]() -> rs_status {
         std::lock_guard<std::mutex> lock(ctx->mu);
         DeviceGuard dg(ctx->device);
         ProfScope prof(ctx);
-        Geom g{S, uint32_t(S / 8)};
-        g.orig_stride = orig_stride;
-        g.rec_stride = rec_stride;
+        const Geom g = device_geom(S, orig_stride, rec_stride, 0, {d_orig, d_rec});
         auto s = static_cast<hipStream_t>(stream);
         if (high)
             encode_high(ctx, ctx->ws(s), g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
@@ -1046,7 +1074,7 @@ rs_status rs_encode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint
     if (!ctx || !ptr_ok(d_orig) || !ptr_ok(d_rec)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     const int high = resolve(rate, N, M, S, err);
     if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
-    if (S % 64 || !stride_ok(orig_stride, S) || !stride_ok(rec_stride, S)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    if (!stride_ok(orig_stride, S) || !stride_ok(rec_stride, S)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     const uint64_t orig_b = orig_stripe_stride ? orig_stripe_stride : N * (orig_stride ? orig_stride : S);
     const uint64_t rec_b = rec_stripe_stride ? rec_stripe_stride : M * (rec_stride ? rec_stride : S);
     if (stripes == 0) return set_err(err, RS_OK);
@@ -1054,9 +1082,8 @@ rs_status rs_encode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint
         std::lock_guard<std::mutex> lock(ctx->mu);
         DeviceGuard dg(ctx->device);
         ProfScope prof(ctx);
-        Geom g{S, uint32_t(S / 8)};
-        g.orig_stride = orig_stride;
-        g.rec_stride = rec_stride;
+        Geom g = device_geom(S, orig_stride, rec_stride, 0, {d_orig, d_rec});
+        if ((orig_b | rec_b) % 4) g.fmt.io_bytes = 1, g.fmt.full_packs = uint32_t(S / 64 * 8), g.fmt.tail_h = uint32_t(S % 64 / 2);
         g.orig_bstride = orig_b;
         g.rec_bstride = rec_b;
         auto s = static_cast<hipStream_t>(stream);
@@ -1102,7 +1129,7 @@ rs_context::Pipe &pipe_of(rs_context *ctx) {
 uint64_t slice_width(uint64_t S, uint32_t slices) {
     const uint64_t blocks = S / 64;
     const uint64_t k = std::max<uint64_t>(1, std::min<uint64_t>(slices ? slices : 1, blocks));
-    return (blocks + k - 1) / k * 64;
+    return std::max<uint64_t>(64, (blocks + k - 1) / k * 64);  // S < 64: one slice (the tail)
 }
 
 // hipMemcpy2DAsync of the rows [r0, r1) where flag[r] == want, in runs
@@ -1140,7 +1167,6 @@ rs_status rs_encode_host(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, 
     if (!ctx || !h_orig || !h_rec) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     const int high = resolve(rate, N, M, S, err);
     if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
-    if (S % 64) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     return guarded(err, [&]() -> rs_status {
         std::lock_guard<std::mutex> lock(ctx->mu);
         DeviceGuard dg(ctx->device);
@@ -1157,8 +1183,7 @@ rs_status rs_encode_host(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, 
             hipStream_t s = P.st[k % rs_context::Pipe::kStreams];
             Workspace &ws = P.ws[k % rs_context::Pipe::kStreams];
             check(hipMemcpy2DAsync(d_o + a, S, h_o + a, S, b - a, N, hipMemcpyHostToDevice, s));
-            Geom g{b - a, uint32_t((b - a) / 8)};
-            g.orig_stride = g.rec_stride = S;
+            const Geom g = device_geom(b - a, S, S, S, {d_o + a, d_r + a});
             if (high) encode_high(ctx, ws, g, N, M, d_o + a, d_r + a, s);
             else encode_low(ctx, ws, g, N, M, d_o + a, d_r + a, s);
             check(hipMemcpy2DAsync(h_r + a, S, d_r + a, S, b - a, M, hipMemcpyDeviceToHost, s));
@@ -1175,7 +1200,6 @@ rs_status rs_decode_host(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, 
         return set_err(err, RS_ERR_INVALID_ARGUMENT);
     const int high = resolve(rate, N, M, S, err);
     if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
-    if (S % 64) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     uint64_t have_o = 0, have_r = 0;
     for (uint64_t i = 0; i < N; ++i) have_o += orig_present[i] != 0;
     for (uint64_t i = 0; i < M; ++i) have_r += rec_present[i] != 0;
@@ -1205,8 +1229,7 @@ rs_status rs_decode_host(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, 
             // only received rows travel in, only restored rows travel out
             copy_rows(d_o + a, h_o + a, S, b - a, orig_present, 1, N, hipMemcpyHostToDevice, s);
             copy_rows(d_r + a, h_r + a, S, b - a, rec_present, 1, M, hipMemcpyHostToDevice, s);
-            Geom g{b - a, uint32_t((b - a) / 8)};
-            g.orig_stride = g.rec_stride = g.out_stride = S;
+            const Geom g = device_geom(b - a, S, S, S, {d_o + a, d_r + a, d_x + a});
             decode_dev(ctx, ws, high, g, N, M, d_o + a, orig_present, d_r + a, rec_present, d_x + a, s);
             copy_rows(h_x + a, d_x + a, S, b - a, orig_present, 0, N, hipMemcpyDeviceToHost, s);
         }
@@ -1223,7 +1246,7 @@ rs_status rs_decode_device_strided(rs_context *ctx, rs_rate rate, uint64_t N, ui
         return set_err(err, RS_ERR_INVALID_ARGUMENT);
     const int high = resolve(rate, N, M, S, err);
     if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
-    if (S % 64 || !stride_ok(orig_stride, S) || !stride_ok(rec_stride, S) || !stride_ok(restored_stride, S))
+    if (!stride_ok(orig_stride, S) || !stride_ok(rec_stride, S) || !stride_ok(restored_stride, S))
         return set_err(err, RS_ERR_INVALID_ARGUMENT);
     uint64_t have_o = 0, have_r = 0;
     for (uint64_t i = 0; i < N; ++i) have_o += orig_present[i] != 0;
@@ -1238,10 +1261,7 @@ rs_status rs_decode_device_strided(rs_context *ctx, rs_rate rate, uint64_t N, ui
         std::lock_guard<std::mutex> lock(ctx->mu);
         DeviceGuard dg(ctx->device);
         ProfScope prof(ctx);
-        Geom g{S, uint32_t(S / 8)};
-        g.orig_stride = orig_stride;
-        g.rec_stride = rec_stride;
-        g.out_stride = restored_stride;
+        const Geom g = device_geom(S, orig_stride, rec_stride, restored_stride, {d_orig, d_rec, d_restored});
         decode_dev(ctx, ctx->ws(static_cast<hipStream_t>(stream)), high, g, N, M, static_cast<const uint8_t *>(d_orig), orig_present,
                    static_cast<const uint8_t *>(d_rec), rec_present, static_cast<uint8_t *>(d_restored),
                    static_cast<hipStream_t>(stream));
@@ -1266,7 +1286,7 @@ rs_status rs_decode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint
         return set_err(err, RS_ERR_INVALID_ARGUMENT);
     const int high = resolve(rate, N, M, S, err);
     if (high < 0) return rs_status(err ? err->code : RS_ERR_UNSUPPORTED_SHARD_COUNT);
-    if (S % 64 || !stride_ok(orig_stride, S) || !stride_ok(rec_stride, S) || !stride_ok(restored_stride, S))
+    if (!stride_ok(orig_stride, S) || !stride_ok(rec_stride, S) || !stride_ok(restored_stride, S))
         return set_err(err, RS_ERR_INVALID_ARGUMENT);
     uint64_t have_o = 0, have_r = 0;
     for (uint64_t i = 0; i < N; ++i) have_o += orig_present[i] != 0;
@@ -1281,13 +1301,12 @@ rs_status rs_decode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint
         std::lock_guard<std::mutex> lock(ctx->mu);
         DeviceGuard dg(ctx->device);
         ProfScope prof(ctx);
-        Geom g{S, uint32_t(S / 8)};
-        g.orig_stride = orig_stride;
-        g.rec_stride = rec_stride;
-        g.out_stride = restored_stride;
+        Geom g = device_geom(S, orig_stride, rec_stride, restored_stride, {d_orig, d_rec, d_restored});
         g.orig_bstride = orig_stripe_stride ? orig_stripe_stride : N * g.orig();
         g.rec_bstride = rec_stripe_stride ? rec_stripe_stride : M * g.rec();
         g.out_bstride = restored_stripe_stride ? restored_stripe_stride : N * g.out();
+        if ((g.orig_bstride | g.rec_bstride | g.out_bstride) % 4)
+            g.fmt.io_bytes = 1, g.fmt.full_packs = uint32_t(S / 64 * 8), g.fmt.tail_h = uint32_t(S % 64 / 2);
         for (uint64_t b0 = 0; b0 < stripes; b0 += kMaxBatchStripes) {  // grid.y limit
             g.stripes = uint32_t(std::min<uint64_t>(kMaxBatchStripes, stripes - b0));
             decode_dev(ctx, ctx->ws(static_cast<hipStream_t>(stream)), high, g, N, M,

@@ -14,6 +14,51 @@ struct RowMap {
     uint32_t row_begin = 0, row_end = 0;
 };
 
+// Byte layout of the caller's shard matrices (src / dst RowMaps; the work
+// buffers always use whole 64-byte blocks).  Shards of any even length S:
+// S / 64 whole blocks (packs 0 .. full_packs - 1 at the usual offsets), then a
+// tail of t = S % 64 bytes holding tail_h = t / 2 low bytes followed by
+// tail_h high bytes -- the reference's tail layout (src/engine/shards.rs:38-74,
+// src/algorithm.md): tail pack p (elements 4p .. 4p + 3 of the last block) has
+// its low bytes at 64 * (full_packs / 8) + 4p, its high bytes tail_h bytes
+// further, and min(4, tail_h - 4p) valid elements.  io_bytes: some caller
+// matrix is not 4-byte aligned (base or row stride); every caller access then
+// goes byte by byte.
+struct ShardFormat {
+    uint32_t full_packs = 0xFFFFFFFFu;  // default: rows of whole 64-byte blocks
+    uint32_t tail_h = 0;
+    uint32_t io_bytes = 0;
+};
+
+// Offsets of pack pk inside a caller row: low word, high word - low word,
+// valid elements, and whether the access must go byte by byte.
+struct PackIO {
+    uint32_t lo, hi_delta, cnt;
+    bool bytes;
+};
+__host__ __device__ inline PackIO pack_io(const ShardFormat &f, uint32_t pk) {
+    if (pk < f.full_packs) return {(pk >> 3) * 64u + (pk & 7u) * 4u, 32u, 4u, f.io_bytes != 0};
+    const uint32_t p = pk - f.full_packs, e = 4u * p;
+    return {(f.full_packs >> 3) * 64u + e, f.tail_h, f.tail_h > e + 4u ? 4u : f.tail_h - e, true};
+}
+__device__ __forceinline__ uint32_t ld_word(const uint8_t *p, const PackIO &io) {
+    if (!io.bytes) return *reinterpret_cast<const uint32_t *>(p);
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < 4; ++e)
+        if (e < io.cnt) v |= uint32_t(p[e]) << (8 * e);
+    return v;
+}
+__device__ __forceinline__ void st_word(uint8_t *p, uint32_t v, const PackIO &io) {
+    if (!io.bytes) {
+        *reinterpret_cast<uint32_t *>(p) = v;
+        return;
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < 4; ++e)
+        if (e < io.cnt) p[e] = uint8_t(v >> (8 * e));
+}
+
 // One pass of the multi-pass transform (see DESIGN.md "Pass structure").
 //
 // A workgroup owns one row SET x one 64-pack column SLICE.  A row set is
@@ -53,6 +98,7 @@ struct PassArgs {
 
     const uint32_t *tw = nullptr;       // perm tables indexed by skew index (zero table = no multiply)
     const uint32_t *lut = nullptr;      // perm tables indexed by log factor
+    ShardFormat fmt;                    // byte layout of src / dst (work buffers: whole blocks)
 
     // ---- 2-level decodes (blk_masks = 1): per block b = row >> blk_shift (b < 256),
     // zero_in bit b: the block's work_in rows are zero (never computed; load as zero);
@@ -112,6 +158,7 @@ struct MonoArgs {
     uint32_t fused_eval = 0, low_rate = 0, end = 0, lw0 = 0;
     // split plan (mono_split(L)): every restored row lies in half out_half of the 2^L work rows
     uint32_t split = 0, out_half = 0;
+    ShardFormat fmt;  // byte layout of src / dst
     const uint16_t *lw_fold = nullptr;
     uint32_t erased[kMonoFusedRows / 32] = {}, received[kMonoFusedRows / 32] = {};
     // a batch of stripes of one shape in one launch (staged kernel, grid.y =

@@ -71,8 +71,9 @@ struct Pass {
 };
 
 struct Ctx {
-    uint32_t g, p, s_lo, s_hi, a, pk_off;
+    uint32_t g, p, s_lo, s_hi, a, pk_off;  // pk_off: the pack's low word in a row (work buffers: high word + 32)
     bool pk_ok;
+    PackIO io;  // the pack in the caller's src / dst rows (tail shards, unaligned matrices)
     __device__ __forceinline__ uint32_t grow(uint32_t j, int K) const { return s_lo + (j << a) + (s_hi << (a + K)); }
 };
 
@@ -274,8 +275,8 @@ __device__ __forceinline__ void load_rows(const PassArgs &A, const Ctx &c, uint3
             uint32_t l = 0, h = 0;
             if (c.pk_ok && r >= m.row_begin && r < m.row_end) {
                 const uint8_t *p = p0 + step * uint64_t(i);
-                l = ld32(p);
-                h = ld32(p + 32);
+                l = ld_word(p, c.io);
+                h = ld_word(p + c.io.hi_delta, c.io);
             }
             lo[i] = l;
             hi[i] = h;
@@ -297,8 +298,13 @@ __device__ __forceinline__ void load_rows(const PassArgs &A, const Ctx &c, uint3
         if (SCALE && (A.rowinfo[r] & 0x10000u)) p = nullptr;
         uint32_t l = 0, h = 0;
         if (p && c.pk_ok) {
-            l = ld32(p + c.pk_off);
-            h = ld32(p + c.pk_off + 32);
+            if (A.work_in) {
+                l = ld32(p + c.pk_off);
+                h = ld32(p + c.pk_off + 32);
+            } else {
+                l = ld_word(p + c.pk_off, c.io);
+                h = ld_word(p + c.pk_off + c.io.hi_delta, c.io);
+            }
         }
         lo[i] = l;
         hi[i] = h;
@@ -352,8 +358,8 @@ __device__ __forceinline__ void store_rows(const PassArgs &A, const Ctx &c, uint
             const uint32_t r = r0 + d * uint32_t(i);
             if (c.pk_ok && r >= m.row_begin && r < m.row_end) {
                 uint8_t *p = p0 + step * uint64_t(i);
-                st32(p, lo[i]);
-                st32(p + 32, hi[i]);
+                st_word(p, lo[i], c.io);
+                st_word(p + c.io.hi_delta, hi[i], c.io);
             }
         });
         return;
@@ -374,8 +380,13 @@ __device__ __forceinline__ void store_rows(const PassArgs &A, const Ctx &c, uint
             }
         }
         if (p && c.pk_ok) {
-            st32(p + c.pk_off, l);
-            st32(p + c.pk_off + 32, h);
+            if (A.work_out) {
+                st32(p + c.pk_off, l);
+                st32(p + c.pk_off + 32, h);
+            } else {
+                st_word(p + c.pk_off, l, c.io);
+                st_word(p + c.pk_off + c.io.hi_delta, h, c.io);
+            }
         }
     });
 }
@@ -611,7 +622,8 @@ __device__ __forceinline__ Ctx make_ctx(const PassArgs &A, uint32_t bx) {
     c.s_hi = set >> A.a;
     const uint32_t pk = slice * P::SP + c.p;
     c.pk_ok = pk < A.packs;
-    c.pk_off = (pk >> 3) * 64u + (pk & 7u) * 4u;
+    c.io = pack_io(A.fmt, pk);
+    c.pk_off = c.io.lo;  // = (pk >> 3) * 64 + (pk & 7) * 4 for every pack
     return c;
 }
 

@@ -590,11 +590,11 @@ __device__ __forceinline__ uint32_t paired_row(uint32_t lane, uint32_t wave, int
 // paired words; finish_col completes them.  Missing rows inside the caller's
 // matrices are read and discarded by the decode's scaling.
 template <int L, int LR, bool SPLIT = false>
-__device__ __forceinline__ void issue_col(const MonoArgs &A, uint32_t chunk, uint32_t pk_off, const StripeBases &sb,
+__device__ __forceinline__ void issue_col(const MonoArgs &A, uint32_t chunk, const PackIO &io, const StripeBases &sb,
                                           uint32_t (&w)[2 << LR], uint32_t lane, uint32_t wave, bool live = true) {
     using S = SeqOf<L, LR, false, SPLIT>;
     const uint32_t base = chunk * (1u << L);
-    const uint32_t half = (lane & 1u) * 32u;
+    const uint32_t off = io.lo + ((lane & 1u) ? io.hi_delta : 0u);
     static_for<0, (2 << LR)>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         const uint32_t r = paired_row<S, 0, LR>(lane, wave, j) + base;
@@ -602,9 +602,9 @@ __device__ __forceinline__ void issue_col(const MonoArgs &A, uint32_t chunk, uin
         uint32_t v = 0;
 #ifdef RS_MONO_SKIP_IO
         p = nullptr;
-        v = r * 0x9E3779B9u + half;
+        v = r * 0x9E3779B9u + off;
 #endif
-        if (p && live) v = *reinterpret_cast<const uint32_t *>(p + pk_off + half);
+        if (p && live) v = ld_word(p + off, io);
         w[j] = v;
     });
 }
@@ -659,10 +659,10 @@ __device__ __forceinline__ void finish_col(uint32_t (&w)[2 << LR], const ScaleTa
 }
 
 template <int L, int LR, bool SCALE>
-__device__ __forceinline__ void load_col(const MonoArgs &A, uint32_t chunk, uint32_t pk_off, const StripeBases &sb,
+__device__ __forceinline__ void load_col(const MonoArgs &A, uint32_t chunk, const PackIO &io, const StripeBases &sb,
                                          Col<L, LR> &c, uint32_t lane, uint32_t wave) {
     uint32_t w[2 << LR];
-    issue_col<L, LR>(A, chunk, pk_off, sb, w, lane, wave);
+    issue_col<L, LR>(A, chunk, io, sb, w, lane, wave);
     ScaleTabs<L, LR> st;
     if constexpr (SCALE) scale_issue<L, LR>(A, A.rowinfo, st, lane, wave);
     finish_col<L, LR, SCALE>(w, &st, c, lane);
@@ -673,7 +673,7 @@ __device__ __forceinline__ void load_col(const MonoArgs &A, uint32_t chunk, uint
 // multiplied by exp(65535 - log factor) (rate_high.rs:241-245).
 template <int L, int LR, bool REVEAL, bool SPLIT = false>
 __device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *rowinfo, uint32_t chunk,
-                                          uint32_t pk_off, const StripeBases &sb, Col<L, LR> &c, uint32_t lane,
+                                          const PackIO &io, const StripeBases &sb, Col<L, LR> &c, uint32_t lane,
                                           uint32_t wave) {
     using S = SeqOf<L, LR, true, SPLIT>;
     constexpr int I = S::v.count;
@@ -706,7 +706,7 @@ __device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *row
         w[2 * i + 1] = c.hi[i];
         xpose<0>(w[2 * i], w[2 * i + 1], lane);
     });
-    const uint32_t half = (lane & 1u) * 32u;
+    const uint32_t off = io.lo + ((lane & 1u) ? io.hi_delta : 0u);
     static_for<0, 2 * R>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         const uint32_t r = paired_row<S, I, LR>(lane, wave, j) + base;
@@ -718,7 +718,7 @@ __device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *row
 #endif
             if (keep) {
                 uint8_t *p = sb.dst + uint64_t(r - A.dst.row_begin) * A.dst.stride;
-                *reinterpret_cast<uint32_t *>(p + pk_off + half) = w[j];
+                st_word(p + off, w[j], io);
             }
         }
     });
@@ -1078,7 +1078,7 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
     if (pk >= A.packs) return;
     const StripeBases sb = BATCH ? stripe_bases(A, blockIdx.y) : StripeBases{A.src[0].base, A.src[1].base,
                                                                              const_cast<uint8_t *>(A.dst.base)};
-    const uint32_t pk_off = (pk >> 3) * 64u + (pk & 7u) * 4u;
+    const PackIO io = pack_io(A.fmt, pk);  // the pack's bytes in the caller's rows (tails: shards.rs:38-74)
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t *img_i = A.img + uint64_t(A.ifft_img) * A.img_words;
@@ -1119,7 +1119,7 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             lw[1] = A.lw_fold[i0 + 1];
         }
         uint32_t w[2 << LR];
-        issue_col<L, LR, SPLIT>(A, 0, pk_off, sb, w, lane, wave, live);
+        issue_col<L, LR, SPLIT>(A, 0, io, sb, w, lane, wave, live);
         // phase-1 tables (a wave that skips phase 1 reads one table: no branch
         // around the loads); B0: layer 0's go into the region first, the
         // layers above when layer 0 has read them (run_seq's hook)
@@ -1253,15 +1253,15 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             run_seq<L, LR, true, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, NoHook{});
         }
         RS_MSTAMP(10);
-        store_col<L, LR, DEC, SPLIT>(A, ri, 0, pk_off, sb, c, lane, wave);
+        store_col<L, LR, DEC, SPLIT>(A, ri, 0, io, sb, c, lane, wave);
         RS_MSTAMP(11);
     } else if constexpr (MODE == kMonoEncodeHigh) {
         // rate_high.rs:44-87: recovery = FFT_0(XOR_c IFFT_{c n + n}(chunk c))
-        load_col<L, LR, false>(A, 0, pk_off, sb, c, lane, wave);
+        load_col<L, LR, false>(A, 0, io, sb, c, lane, wave);
         run_seq<L, LR, false, kMonoPrefetch>(GlobalTabs{img_i}, c, plane, lane, wave, NoHook{});
         for (uint32_t ch = 1; ch < A.chunks; ++ch) {
             C t;
-            load_col<L, LR, false>(A, ch, pk_off, sb, t, lane, wave);
+            load_col<L, LR, false>(A, ch, io, sb, t, lane, wave);
             run_seq<L, LR, false, kMonoPrefetch>(
                 GlobalTabs{img_i + uint64_t(ch) * A.ifft_img_step * A.img_words}, t, plane, lane, wave, NoHook{});
             static_for<0, R>([&](auto ic) {
@@ -1270,24 +1270,24 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             });
         }
         run_seq<L, LR, true, kMonoPrefetch>(GlobalTabs{img_f}, c, plane, lane, wave, NoHook{});
-        store_col<L, LR, false>(A, A.rowinfo, 0, pk_off, sb, c, lane, wave);
+        store_col<L, LR, false>(A, A.rowinfo, 0, io, sb, c, lane, wave);
     } else if constexpr (MODE == kMonoEncodeLow) {
         // rate_low.rs:44-87: recovery chunk c = FFT_{c n + n}(IFFT_0(original))
-        load_col<L, LR, false>(A, 0, pk_off, sb, c, lane, wave);
+        load_col<L, LR, false>(A, 0, io, sb, c, lane, wave);
         run_seq<L, LR, false, kMonoPrefetch>(GlobalTabs{img_i}, c, plane, lane, wave, NoHook{});
         for (uint32_t ch = 0; ch < A.chunks; ++ch) {
             C t = c;
             run_seq<L, LR, true, kMonoPrefetch>(
                 GlobalTabs{img_f + uint64_t(ch) * A.fft_img_step * A.img_words}, t, plane, lane, wave, NoHook{});
-            store_col<L, LR, false>(A, A.rowinfo, ch, pk_off, sb, t, lane, wave);
+            store_col<L, LR, false>(A, A.rowinfo, ch, io, sb, t, lane, wave);
         }
     } else {
         // rate_high.rs:213-245 / rate_low.rs:213-245 after eval_poly
-        load_col<L, LR, true>(A, 0, pk_off, sb, c, lane, wave);
+        load_col<L, LR, true>(A, 0, io, sb, c, lane, wave);
         run_seq<L, LR, false, kMonoPrefetch>(GlobalTabs{img_i}, c, plane, lane, wave, NoHook{});
         formal_derivative<L, LR>(c, plane, lane, wave);
         run_seq<L, LR, true, kMonoPrefetch>(GlobalTabs{img_f}, c, plane, lane, wave, NoHook{});
-        store_col<L, LR, true>(A, A.rowinfo, 0, pk_off, sb, c, lane, wave);
+        store_col<L, LR, true>(A, A.rowinfo, 0, io, sb, c, lane, wave);
     }
 }
 

@@ -703,7 +703,9 @@ def test_column_kernel_and_pass_paths_match_oracle(torch, rs, rate, N, M, S, mon
 
 @pytest.mark.parametrize("rate,N,M,S,slices,pinned", [
     ("default", 1024, 1024, 1024, 4, True), ("default", 1024, 1024, 1024, 1, False), ("high", 3000, 700, 640, 3, True),
-    ("low", 100, 1000, 192, 8, False), ("default", 5000, 300, 4096, 5, True)])
+    ("low", 100, 1000, 192, 8, False), ("default", 5000, 300, 4096, 5, True),
+    # shards with a tail block: the last slice carries it (34 bytes alone for 130 / 2)
+    ("default", 1000, 1000, 130, 2, True), ("high", 300, 50, 1000, 3, False), ("low", 50, 300, 6, 4, True)])
 def test_host_pipeline_matches_oracle(torch, rs, rate, N, M, S, slices, pinned):
     orig = O.generate_original(N, S, 21)
     want = O.encode(rate, orig, M)
@@ -912,3 +914,113 @@ def test_bound_device_calls_match_oracle(torch, rs):
     assert np.array_equal(got[N - L:], orig[N - L:]) and np.all(got[:N - L] == 0x33)
     with pytest.raises(rs.Error):
         rs.encode_device_call(3, 70000, 64, d_orig, d_rec)()
+
+
+# ---------------------------------------------------------------------------
+# device path on shards of any even length (rs_device.hpp ShardFormat): the tail
+# block keeps the reference's layout (shards.rs:38-74), so the device result must
+# equal the oracle's (which re-packs like the reference) byte for byte, and the
+# reference's golden vectors must hash equal through the device path too.
+
+def _device_golden(torch, rs, c):
+    n, m, s = c["original_count"], c["recovery_count"], c["shard_bytes"]
+    orig = O.generate_original(n, s, c["seed"])
+    d_o = _dev(torch, orig)
+    d_r = torch.full((m, s), 0xEE, dtype=torch.uint8, device="cuda")
+    rs.encode_device(n, m, s, d_o, d_r, rate_=RATE[c["rate"]])
+    torch.cuda.synchronize()
+    rec = d_r.cpu().numpy()
+    assert hashlib.sha256(rec.tobytes()).hexdigest() == c["recovery_sha256"], c["source"]
+    op = np.zeros(n, np.uint8)
+    rp = np.zeros(m, np.uint8)
+    for a, b in c["decoder_original"]:
+        op[a:b] = 1
+    for a, b in c["decoder_recovery"]:
+        rp[a:b] = 1
+    if op.all():
+        return
+    d_oo = _dev(torch, np.where(op[:, None] == 1, orig, 0xA5).astype(np.uint8))
+    d_rr = _dev(torch, np.where(rp[:, None] == 1, rec, 0x5A).astype(np.uint8))
+    d_out = torch.full((n, s), 0x33, dtype=torch.uint8, device="cuda")
+    rs.decode_device(n, m, s, d_oo, op, d_rr, rp, d_out, rate_=RATE[c["rate"]])
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    miss = op == 0
+    assert np.array_equal(out[miss], orig[miss]), c["source"]
+    assert np.all(out[~miss] == 0x33)
+
+
+@pytest.mark.parametrize("case", [pytest.param(c, id=c["name"]) for c in GOLD["single"]
+                                  if not c["name"].startswith(("DEFAULT_TINY", "LOW_TINY"))])
+def test_golden_vectors_device_path(torch, rs, case):
+    """Every golden case (HIGH_34000_2000_s8 / LOW_2000_34000_s8: 8-byte shards, all tail) via the device API."""
+    _device_golden(torch, rs, case)
+
+
+TAIL_SIZES = [2, 4, 6, 30, 32, 34, 62, 64, 66, 126, 128, 130]
+
+
+@pytest.mark.parametrize("S", TAIL_SIZES)
+@pytest.mark.parametrize("rate,N,M", [("default", 3, 2), ("high", 1000, 100), ("low", 100, 1000),
+                                      ("default", 4096, 4096), ("high", 20000, 3000)])
+def test_device_path_any_even_shard_size(torch, rs, rate, N, M, S):
+    """decoder_result.rs:166-171 sizes through rs_encode_device / rs_decode_device (column kernel and passes)."""
+    orig = O.generate_original(N, S, S)
+    want = O.encode(rate, orig, M)
+    got = gpu_encode(torch, rs, rate, orig, M)
+    assert np.array_equal(got, want)
+    rng = np.random.default_rng(S + N)
+    L = max(1, min(N, M) // 4)
+    op = np.ones(N, np.uint8)
+    op[rng.choice(N, L, replace=False)] = 0
+    rp = np.zeros(M, np.uint8)
+    rp[rng.choice(M, L, replace=False)] = 1
+    out = gpu_decode(torch, rs, rate, orig, op, want, rp)
+    miss = op == 0
+    assert np.array_equal(out[miss], orig[miss])
+    assert np.all(out[~miss] == 0x33)
+
+
+@pytest.mark.parametrize("S,off,pad", [(64, 1, 3), (130, 2, 0), (34, 1, 1), (1024, 3, 5), (6, 0, 1)])
+@pytest.mark.parametrize("rate,N,M", [("default", 1000, 1000), ("high", 3000, 300), ("low", 64, 64)])
+def test_device_path_unaligned_matrices(torch, rs, rate, N, M, S, off, pad):
+    """Row strides / base addresses that are not multiples of 4 go byte by byte; same bytes as the oracle."""
+    orig = O.generate_original(N, S, 9)
+    want = O.encode(rate, orig, M)
+    W = S + off + pad
+    d_ob = torch.full((N, W), 0x11, dtype=torch.uint8, device="cuda")
+    d_ob[:, off:off + S] = _dev(torch, orig)
+    d_rb = torch.full((M, W), 0xEE, dtype=torch.uint8, device="cuda")
+    rs.encode_device(N, M, S, d_ob[:, off:off + S], d_rb[:, off:off + S], rate_=RATE[rate])
+    torch.cuda.synchronize()
+    rb = d_rb.cpu().numpy()
+    assert np.array_equal(rb[:, off:off + S], want)
+    assert np.all(rb[:, :off] == 0xEE) and np.all(rb[:, off + S:] == 0xEE), "bytes around the slice must not change"
+    rng = np.random.default_rng(N + S)
+    L = max(1, min(N, M) // 3)
+    op = np.ones(N, np.uint8)
+    op[rng.choice(N, L, replace=False)] = 0
+    rp = np.zeros(M, np.uint8)
+    rp[rng.choice(M, L, replace=False)] = 1
+    d_xb = torch.full((N, W), 0x33, dtype=torch.uint8, device="cuda")
+    rs.decode_device(N, M, S, d_ob[:, off:off + S], op, d_rb[:, off:off + S], rp, d_xb[:, off:off + S],
+                     rate_=RATE[rate])
+    torch.cuda.synchronize()
+    xb = d_xb.cpu().numpy()
+    miss = op == 0
+    assert np.array_equal(xb[miss, off:off + S], orig[miss])
+    assert np.all(xb[~miss] == 0x33)
+    assert np.all(xb[:, :off] == 0x33) and np.all(xb[:, off + S:] == 0x33)
+
+
+@pytest.mark.parametrize("rate,N,M,S,B", [("default", 1024, 1024, 130, 3), ("low", 100, 1000, 34, 2),
+                                          ("default", 64, 64, 1000, 4)])
+def test_batch_with_tail_shards(torch, rs, rate, N, M, S, B):
+    origs = [O.generate_original(N, S, 60 + b) for b in range(B)]
+    d_o = _dev(torch, np.stack(origs))
+    d_r = torch.full((B, M, S), 0xEE, dtype=torch.uint8, device="cuda")
+    rs.encode_device_batch(N, M, S, d_o, d_r, rate_=RATE[rate])
+    torch.cuda.synchronize()
+    got = d_r.cpu().numpy()
+    for b in range(B):
+        assert np.array_equal(got[b], O.encode(rate, origs[b], M)), f"stripe {b}"
