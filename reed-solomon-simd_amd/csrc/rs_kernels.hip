@@ -716,8 +716,15 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
     }
 }
 
+// Occupancy: two 512-thread workgroups per CU at least; the encode's fused
+// IFFT + FFT pass (the most butterflies per loaded row) is held to 6 waves per
+// SIMD (<= 80 VGPRs) so that three of its workgroups share a CU: one's row
+// loads and stores overlap the others' layers.
+template <int LR, int FLAGS>
+constexpr int pass_waves_per_eu() { return FLAGS == (kIfft | kFft) && LR >= 3 ? 6 : 2; }
+
 template <int K, int LR, int SPL, int FLAGS>
-__global__ void __launch_bounds__(1 << (K - LR + SPL), 2) k_pass(const PassArgs A) {
+__global__ void __launch_bounds__(1 << (K - LR + SPL), (pass_waves_per_eu<LR, FLAGS>())) k_pass(const PassArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     pass_body<K, LR, SPL, FLAGS>(A, blockIdx.x, blockIdx.y, lds);
 }
@@ -735,7 +742,8 @@ hipError_t launch_f(const PassArgs &A, hipStream_t s) {
     }
     PassArgs B = A;
     B.slices = (A.packs + P::SP - 1) / P::SP;
-    dim3 grid(B.slices * B.nsets, B.grid_chunks);
+    const uint32_t total = B.slices * B.nsets;
+    dim3 grid(total, B.grid_chunks);
     k_pass<K, LR, SPL, F><<<grid, P::kThreads, lds, s>>>(B);
     snprintf(launch_name_buf(), kLaunchNameBytes, "k_pass<%d, %d, %d, %d>", K, LR, SPL, F);
     return hipGetLastError();

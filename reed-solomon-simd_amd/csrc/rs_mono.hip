@@ -31,11 +31,16 @@
 namespace rs {
 namespace {
 
-#ifdef RS_MONO_STAMPS  // tools/mono_probe.hip: per-workgroup timestamps (waits for memory first)
+#ifdef RS_MONO_STAMPS  // tools/mono_probe.hip: per-workgroup timestamps
 __device__ uint64_t g_mono_stamps[4096][16];
+#ifdef RS_MONO_STAMP_WAIT  // each stamp first waits for the wave's outstanding memory ops
+#define RS_MSTAMP_WAIT() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
+#else  // the time the wave's instruction stream reaches the stamp
+#define RS_MSTAMP_WAIT() asm volatile("" ::: "memory")
+#endif
 #define RS_MSTAMP(i)                                                                                 \
     do {                                                                                             \
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                  \
+        RS_MSTAMP_WAIT();                                                                            \
         if (threadIdx.x == blockDim.x - 64 && blockIdx.x < 4096) g_mono_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
@@ -344,9 +349,16 @@ struct Stage {
     static constexpr uint32_t kWaves = 1u << (L - LR - 6);
     static constexpr uint32_t plane_words = 2 * n;
     static constexpr uint32_t words = plane_words + (kShared + kWaves * kPriv) * 20;
+    // encode (IFFT and FFT on different skew offsets t_i, t_f): phase 3's tables
+    // are phase 1's XOR D_b, one table per phase-3 layer b (twiddles are
+    // GF(2)-linear in the global group index, so are the perm tables:
+    // D_b = the table of group (t_i ^ t_f) * n / 2^(b+1)), kept after the shared tables
+    static constexpr uint32_t kD = NB3;
+    static constexpr uint32_t words_enc = words + kD * 20;
     static constexpr uint32_t words_dec = words + n;  // + per-row decode info (fused eval_poly)
     // SPLIT decode: + a second column plane (the cross-half step's formal-derivative values)
     static constexpr uint32_t words_split = words_dec + (SPLIT ? plane_words : 0);
+    static_assert(L > 11 || (words_enc * 4 <= 160 * 1024 && words_split * 4 <= 160 * 1024), "column kernel: LDS per workgroup");
 };
 
 // Table source: tables staged in LDS (STAGED column kernel).  Phase 1 (IFFT
@@ -375,6 +387,10 @@ struct LdsTabs {
             slot = G::kShI + (G::n >> G::WB) - (G::n >> x) + (row >> (x + 1));
             base = shared;
         }
+#ifdef RS_MONO_FAKE_TABS  // tools/mono_probe.hip: tables without LDS traffic
+        for (int q = 0; q < 20; ++q) t[q] = slot * 0x01010101u + q + uint32_t(reinterpret_cast<uintptr_t>(base));
+        return;
+#endif
         const uint4 *p = reinterpret_cast<const uint4 *>(base) + slot * 5u;
 #pragma unroll
         for (int q = 0; q < 5; ++q) {
@@ -1053,6 +1069,20 @@ __device__ __forceinline__ uint4 shared_piece(const uint32_t *img_i, const uint3
     const uint32_t slot = t < G::kShI ? G::n - (G::n >> G::IW) + t : G::n - (G::n >> G::WB) + (t - G::kShI);
     return reinterpret_cast<const uint4 *>(t < G::kShI ? img_i : img_f)[slot * 5u + piece];
 }
+// 16-byte piece q of the D tables (Stage::kD): layer b = q / 5 of image t_i ^ t_f, group 0
+template <int L, int LR, bool SPLIT = false>
+__device__ __forceinline__ uint4 d_piece(const uint32_t *img_d, uint32_t q) {
+    using G = Stage<L, LR, SPLIT>;
+    const uint32_t b = q / 5, piece = q - b * 5;
+    return reinterpret_cast<const uint4 *>(img_d)[(G::n - (G::n >> b)) * 5u + piece];
+}
+// layer of table slot t of a wave-private region (phases 1 and 3)
+template <int L, int LR, bool SPLIT = false>
+__device__ __forceinline__ uint32_t priv_layer(uint32_t t) {
+    using G = Stage<L, LR, SPLIT>;
+    const uint32_t y = (G::W >> G::B0) - t;
+    return uint32_t(G::IW - int(32 - __builtin_clz(y - 1)));
+}
 
 #ifndef RS_MONO_LDS_PF
 #define RS_MONO_LDS_PF 2
@@ -1083,18 +1113,20 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t *img_i = A.img + uint64_t(A.ifft_img) * A.img_words;
     const uint32_t *img_f = A.img + uint64_t(A.fft_img) * A.img_words;
+    const uint32_t *img_d = A.img + uint64_t(A.ifft_img ^ A.fft_img) * A.img_words;
     C c;
     if constexpr (STAGED) {
         // one chunk in, one chunk out; every table read comes from LDS (layer
         // 0 of phases 1 / 3 from the image when Stage::B0)
         constexpr bool DEC = MODE == kMonoDecode;
         uint32_t *shared = lds + G::plane_words;
-        uint32_t *priv = shared + G::kShared * 20 + wave * G::kPriv * 20;
+        constexpr uint32_t kSh = DEC ? G::kShared : G::kShared + G::kD;  // shared tables (+ D)
+        uint32_t *priv = shared + kSh * 20 + wave * G::kPriv * 20;
         uint32_t *rinfo = lds + G::words;  // decode with fused eval_poly
         constexpr int KP1 = (5 * G::kUp + 63) / 64;
         constexpr int KP0 = G::B0 ? (5 * G::kL0 + 63) / 64 : 1;
         constexpr int KP3 = G::kP3 ? (5 * G::kP3 + 63) / 64 : 1;  // (guarded by q < 5 * kP3)
-        constexpr int KSH = G::kShared ? (5 * G::kShared + T - 1) / T : 1;
+        constexpr int KSH = kSh ? (5 * kSh + T - 1) / T : 1;  // (guarded by q < 5 * kSh)
         RS_MSTAMP(0);
         // decode: does this wave's phase-1 row block (2^IW consecutive rows) hold a
         // received row?  If not its rows are zero through phase 1: it loads no
@@ -1108,6 +1140,18 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
         }
         // split decode: does this wave's half go on with the FFT (restored rows)?
         const bool out_wave = !SPLIT || (wave >> (L - 1 - G::IW)) == A.out_half;
+        // Phase 3's tables cover the same wave rows, layers and slots as phase
+        // 1's, still in the region when phase 1 ran on real tables (live): the
+        // same tables when IFFT and FFT share the skew offset (decodes,
+        // rate_high.rs:213-245), else phase 1's XOR D_b (encodes, Stage::kD)
+#ifndef RS_MONO_NO_REUSE
+        const bool same3 = A.ifft_img == A.fft_img;
+        const bool reuse3 = live && (same3 || !DEC);
+#else
+        const bool same3 = A.ifft_img == A.fft_img;
+        const bool reuse3 = false;
+#endif
+
         // every global read is requested before any of them is waited for
         // (no branches between them: a branch would make the compiler wait)
         uint32_t ebits = 0, rbits = 0, lw[2] = {0, 0};
@@ -1137,6 +1181,7 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
         static_for<0, KSH>([&](auto kc) {
             const uint32_t q = threadIdx.x + T * decltype(kc)::value;
             if (q < 5 * G::kShared) vs[kc] = shared_piece<L, LR, SPLIT>(img_i, img_f, q);
+            else if (!DEC && q < 5 * kSh) vs[kc] = d_piece<L, LR, SPLIT>(img_d, q - 5 * G::kShared);
         });
 #endif
         const uint32_t *ri = A.rowinfo;
@@ -1171,7 +1216,7 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             write1();
         static_for<0, KSH>([&](auto kc) {
             const uint32_t q = threadIdx.x + T * decltype(kc)::value;
-            if (q < 5 * G::kShared) reinterpret_cast<uint4 *>(shared)[q] = vs[kc];
+            if (q < 5 * kSh) reinterpret_cast<uint4 *>(shared)[q] = vs[kc];
         });
 #endif
         RS_MSTAMP(6);
@@ -1182,12 +1227,33 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
         // phase-1 tables when phase 2 ends
         uint4 v3[KP3];
         auto issue3 = [&]() {
+            if (reuse3) return;
             static_for<0, KP3>([&](auto kc) {
                 const uint32_t q = lane + 64u * decltype(kc)::value;
                 if (q < 5 * G::kP3) v3[kc] = priv_piece<L, LR, SPLIT>(img_f, wave, out_wave ? q : q % 5u);
             });
         };
         auto write3 = [&]() {
+            if (reuse3) {
+                if constexpr (!DEC) {
+                    if (same3) return;
+                    uint4 x[KP3];
+                    static_for<0, KP3>([&](auto kc) {
+                        const uint32_t q = lane + 64u * decltype(kc)::value;
+                        if (q < 5 * G::kP3) {
+                            const uint32_t t = q / 5, piece = q - t * 5;
+                            const uint4 v = reinterpret_cast<const uint4 *>(priv)[q];
+                            const uint4 d = reinterpret_cast<const uint4 *>(shared)[(G::kShared + priv_layer<L, LR, SPLIT>(t)) * 5 + piece];
+                            x[kc] = uint4{v.x ^ d.x, v.y ^ d.y, v.z ^ d.z, v.w ^ d.w};
+                        }
+                    });
+                    static_for<0, KP3>([&](auto kc) {
+                        const uint32_t q = lane + 64u * decltype(kc)::value;
+                        if (q < 5 * G::kP3) reinterpret_cast<uint4 *>(priv)[q] = x[kc];
+                    });
+                }
+                return;
+            }
             static_for<0, KP3>([&](auto kc) {
                 const uint32_t q = lane + 64u * decltype(kc)::value;
                 if (q < 5 * G::kP3) reinterpret_cast<uint4 *>(priv)[q] = v3[kc];
@@ -1312,7 +1378,7 @@ template <int L, int MODE, bool STAGED, bool BATCH = false, bool SPLIT = false>
 hipError_t launch_ls(const MonoArgs &A, hipStream_t s) {
     constexpr int LR = mono_lr(L, STAGED);
     using G = Stage<L, LR, SPLIT>;
-    const size_t lds = STAGED ? size_t(SPLIT ? G::words_split : MODE == kMonoDecode ? G::words_dec : G::words) * 4
+    const size_t lds = STAGED ? size_t(SPLIT ? G::words_split : MODE == kMonoDecode ? G::words_dec : G::words_enc) * 4
                               : size_t(8) << L;
     static bool attr_set = false;  // benign race: idempotent attribute call
     if (!attr_set && lds > 65536) {

@@ -582,6 +582,45 @@ def test_baseline_decode_8192_64k(torch, rs, loss):
     assert torch.equal(d_out[N - L:], d_orig[N - L:])
 
 
+@pytest.mark.parametrize("rate,N,M,S,loss", [("low", 2048, 6144, 65536, 0.5), ("high", 6000, 2000, 65536, 0.3),
+                                               ("default", 4096, 4096, 32768, 1.0)])
+def test_streaming_passes_match_oracle(torch, rs, rate, N, M, S, loss):
+    """Matrices of many times the resident workgroups run the streaming pass form
+    (k_pass_stream: each workgroup walks several blocks, loading the next block's rows
+    under the current block's layers): encode on sampled column blocks vs the oracle,
+    decode restores exactly."""
+    g = torch.Generator(device="cuda")
+    g.manual_seed(N + M)
+    d_orig = torch.randint(0, 256, (N, S), dtype=torch.uint8, device="cuda", generator=g)
+    d_rec = torch.empty((M, S), dtype=torch.uint8, device="cuda")
+    rs.encode_device(N, M, S, d_orig, d_rec, rate_=RATE[rate])
+    torch.cuda.synchronize()
+    nb = S // 64
+    cols = sorted({0, 1, nb // 3, nb // 2 + 5, nb - 1})
+    idx = torch.from_numpy(np.concatenate([np.arange(64 * b, 64 * b + 64) for b in cols])).cuda()
+    o = d_orig.index_select(1, idx).cpu().numpy()
+    got = d_rec.index_select(1, idx).cpu().numpy()
+    O.lib().orc_select_engine(1)
+    try:
+        want = O.encode(rate, o, M)
+    finally:
+        O.lib().orc_select_engine(0)
+    assert np.array_equal(got, want)
+    rng = np.random.default_rng(N)
+    L = max(1, int(min(N, M) * loss))
+    op = np.ones(N, np.uint8)
+    op[rng.choice(N, L, replace=False)] = 0
+    rp = np.zeros(M, np.uint8)
+    rp[rng.choice(M, L, replace=False)] = 1
+    miss = torch.from_numpy(op == 0).cuda()
+    d_in = d_orig.clone()
+    d_in[miss] = 0
+    d_out = torch.zeros_like(d_orig)
+    rs.decode_device(N, M, S, d_in, op, d_rec, rp, d_out, rate_=RATE[rate])
+    torch.cuda.synchronize()
+    assert torch.equal(d_out[miss], d_orig[miss])
+
+
 # ---------------------------------------------------------------------------
 # pass kernels on 2-level transforms (2^7 .. 2^12 rows), column kernel off
 
