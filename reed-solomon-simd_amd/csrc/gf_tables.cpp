@@ -56,6 +56,39 @@ void fill_perm(uint32_t *w, F f) {
         }
 }
 
+// 2-element format (kPerm2Words = 16 words): a word holds the low bytes of 2
+// elements in bytes 0-1 and their high bytes in bytes 2-3.  For each 2-bit
+// field f (bits 2f, 2f+1) of an input byte, two v_perm_b32 tables of 8 bytes:
+//   words [4f, 4f+1]   "direct": bytes 0-3 = low output byte of the LOW-byte
+//                       field's 4 values, bytes 4-7 = high output byte of the
+//                       HIGH-byte field's (selector [lo0 lo1 hi0+4 hi1+4])
+//   words [4f+2, 4f+3] "cross":  bytes 0-3 = low output byte of the HIGH-byte
+//                       field, bytes 4-7 = high output byte of the LOW-byte
+//                       field (selector of the word rotated by 16 bits)
+// (v_perm_b32 S0, S1: selector bytes 0-3 pick S1's bytes, 4-7 S0's, so the
+// first word of each pair is S1).
+template <typename F>
+void fill_perm2(uint32_t *w, F f) {
+    for (int fld = 0; fld < 4; ++fld) {
+        uint8_t direct[8], cross[8];
+        for (int v = 0; v < 4; ++v) {
+            const uint16_t plo = f(static_cast<uint16_t>(v << (2 * fld)));      // low-byte field
+            const uint16_t phi = f(static_cast<uint16_t>(v << (8 + 2 * fld)));  // high-byte field
+            direct[v] = static_cast<uint8_t>(plo & 0xFF);
+            direct[4 + v] = static_cast<uint8_t>(phi >> 8);
+            cross[v] = static_cast<uint8_t>(phi & 0xFF);
+            cross[4 + v] = static_cast<uint8_t>(plo >> 8);
+        }
+        auto word = [](const uint8_t *b) {
+            return b[0] | (b[1] << 8) | (b[2] << 16) | (static_cast<uint32_t>(b[3]) << 24);
+        };
+        w[4 * fld + 0] = word(direct);
+        w[4 * fld + 1] = word(direct + 4);
+        w[4 * fld + 2] = word(cross);
+        w[4 * fld + 3] = word(cross + 4);
+    }
+}
+
 GfTables *build() {
     auto *T = new GfTables;
     T->exp.assign(kOrder, 0);
@@ -117,6 +150,17 @@ GfTables *build() {
         const uint16_t lm = T->skew[idx];
         if (lm == kModulus) continue;  // multiply-by-zero: all-zero table
         std::copy_n(&T->perm_by_log[size_t(lm) * kPermWords], kPermWords, &T->perm_by_skew[size_t(idx) * kPermWords]);
+    }
+    T->perm2_by_log.assign(size_t(kOrder) * kPerm2Words, 0);
+    T->perm2_by_skew.assign(size_t(kOrder) * kPerm2Words, 0);
+    for (uint32_t lm = 0; lm < kOrder; ++lm)
+        fill_perm2(&T->perm2_by_log[size_t(lm) * kPerm2Words],
+                   [&](uint16_t x) { return T->mul(x, static_cast<uint16_t>(lm)); });
+    for (uint32_t idx = 0; idx < kOrder; ++idx) {
+        const uint16_t lm = T->skew[idx];
+        if (lm == kModulus) continue;
+        std::copy_n(&T->perm2_by_log[size_t(lm) * kPerm2Words], kPerm2Words,
+                    &T->perm2_by_skew[size_t(idx) * kPerm2Words]);
     }
     return T;
 }

@@ -14,6 +14,9 @@ constexpr uint32_t kModulus = 65535;
 
 // Number of 32-bit words of one byte-permute multiply table (see PermTable).
 constexpr int kPermWords = 20;
+// Words of one table of the 2-element format (fill_perm2): a 32-bit word holds
+// the low and the high byte of 2 elements, [lo0 lo1 hi0 hi1].
+constexpr int kPerm2Words = 16;
 
 struct GfTables {
     std::vector<uint16_t> exp;        // 65536, exp[65535] == exp[0]
@@ -30,6 +33,9 @@ struct GfTables {
     //                           engine_naive.rs:64-67 / 96-99)
     std::vector<uint32_t> perm_by_log;
     std::vector<uint32_t> perm_by_skew;
+    // the same maps in the 2-element format (kPerm2Words words per entry)
+    std::vector<uint32_t> perm2_by_log;
+    std::vector<uint32_t> perm2_by_skew;
 
     uint16_t mul(uint16_t x, uint16_t log_m) const;
 };

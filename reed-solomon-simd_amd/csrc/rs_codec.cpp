@@ -172,8 +172,15 @@ struct rs_context {
     bool split = true;            // RS_MI355X_NO_SPLIT=1 disables the split decode plan (A/B)
     bool mono_all = false;        // RS_MI355X_MONO_ALL=1: unstaged column kernel too (see use_mono)
     uint32_t mono_max_packs = 256;   // column kernel only up to this many packs (RS_MI355X_MONO_MAX_PACKS)
-    std::mutex img_mu;            // guards d_img
-    uint32_t *d_img[13] = {};     // column-kernel twiddle images per L (built on first use)
+    // 2-element packs (rs_mono.hip Fmt<2>) for staged column-kernel decodes of at
+    // most this many 4-element packs (RS_MI355X_E2_MAX_PACKS; 0 = never), and
+    // for encodes too when e2_encode (measured: tools/e2_probe.py)
+    uint32_t e2_max_packs = 192;
+    bool e2_encode = false;
+    uint32_t *d_lut2 = nullptr;   // perm2_by_log: the 2-element form of d_lut
+    std::mutex img_mu;            // guards d_img, d_img2
+    uint32_t *d_img[13] = {};     // column-kernel twiddle images per L (built at context creation)
+    uint32_t *d_img2[13] = {};    // the same in the 2-element table format
     std::mutex host_engine_mu;  // guards host_engine_buf (rs_engine_*_host staging)
     DevBuf host_engine_buf;
     std::mutex mu;  // guards ws_by_stream (device-resident API scratch), prof, recs
@@ -362,12 +369,15 @@ void run_level(rs::PassArgs A, const Levels &lv, uint32_t k, int flags, uint32_t
 // every skew offset t * n, t = 0 .. 65536/n - 1 (rs_device.hpp), built on the
 // host from the skew tables once per context and L.
 constexpr uint32_t kMonoMinL = 7, kMonoMaxL = 12;
-const uint32_t *mono_images(rs_context *ctx, uint32_t L) {
+const uint32_t *mono_images(rs_context *ctx, uint32_t L, uint32_t elems = 4) {
     std::lock_guard<std::mutex> lock(ctx->img_mu);
-    if (ctx->d_img[L]) return ctx->d_img[L];
+    uint32_t *&slot_ptr = elems == 2 ? ctx->d_img2[L] : ctx->d_img[L];
+    if (slot_ptr) return slot_ptr;
     const rs::GfTables &T = rs::tables();
+    const std::vector<uint32_t> &src = elems == 2 ? T.perm2_by_skew : T.perm_by_skew;
+    const size_t tw = elems == 2 ? rs::kPerm2Words : rs::kPermWords;
     const uint32_t n = 1u << L, nimg = 65536u / n;  // skew offsets t * n + (n - 2) <= 65534
-    const size_t words = size_t(n - 1) * rs::kPermWords;
+    const size_t words = size_t(n - 1) * tw;
     std::vector<uint32_t> h(words * nimg);
     for (uint32_t t = 0; t < nimg; ++t) {
         uint32_t *dst = &h[t * words];
@@ -375,14 +385,13 @@ const uint32_t *mono_images(rs_context *ctx, uint32_t L) {
             for (uint32_t g = 0; g < (n >> (b + 1)); ++g) {
                 const uint32_t slot = n - (n >> b) + g;
                 const uint32_t idx = (g << (b + 1)) + (1u << b) + t * n - 1;
-                std::copy_n(&T.perm_by_skew[size_t(idx) * rs::kPermWords], rs::kPermWords,
-                            dst + size_t(slot) * rs::kPermWords);
+                std::copy_n(&src[size_t(idx) * tw], tw, dst + size_t(slot) * tw);
             }
     }
     uint32_t *d = nullptr;
     check(hipMalloc(&d, h.size() * 4));
     check(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-    ctx->d_img[L] = d;
+    slot_ptr = d;
     return d;
 }
 
@@ -394,14 +403,22 @@ bool use_mono(rs_context *ctx, uint32_t L, const Geom &g, uint32_t chunks) {
     return ctx->mono_all || rs::mono_staged(int(L), chunks);
 }
 
-rs::MonoArgs mono_args(rs_context *ctx, uint32_t L, const Geom &g) {
+// Staged decodes of few packs use 2-element packs: twice the workgroups on
+// a chip whose CUs the 4-element packs leave idle (rs_mono.hip Fmt).  The
+// headline encode measured slower that way (9.4 vs 8.4 us per launch), the
+// decode faster (14.6 vs 15.4 us), hence decodes only by default.
+rs::MonoArgs mono_args(rs_context *ctx, uint32_t L, const Geom &g, bool staged, bool decode = false) {
     rs::MonoArgs M;
-    M.packs = g.packs;
-    M.packs_per_xcd = (g.packs + 7) / 8;
+    const bool e2 = staged && (decode || ctx->e2_encode) && g.packs <= ctx->e2_max_packs && L <= 11;
+    M.elems = e2 ? 2 : 4;
+    // 2-element packs: two per 4-element pack of the whole blocks, one per 2 tail elements
+    M.packs = !e2 ? g.packs
+                  : g.fmt.full_packs == 0xFFFFFFFFu ? 2 * g.packs : 2 * g.fmt.full_packs + (g.fmt.tail_h + 1) / 2;
+    M.packs_per_xcd = (M.packs + 7) / 8;
     M.stripes = g.stripes;  // a batch of stripes runs in one launch
-    M.img = mono_images(ctx, L);
-    M.img_words = uint64_t((1u << L) - 1) * rs::kPermWords;
-    M.lut = ctx->d_lut;
+    M.img = mono_images(ctx, L, M.elems);
+    M.img_words = uint64_t((1u << L) - 1) * (e2 ? rs::kPerm2Words : rs::kPermWords);
+    M.lut = e2 ? ctx->d_lut2 : ctx->d_lut;
     M.fmt = g.fmt;
     return M;
 }
@@ -433,7 +450,7 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
     A.ifft_delta_step = n;
     const rs::RowMap src{orig, g.orig(), 0, uint32_t(N)}, dst{rec, g.rec(), 0, uint32_t(M)};
     if (use_mono(ctx, L, g, C)) {
-        rs::MonoArgs Mo = mono_args(ctx, L, g);
+        rs::MonoArgs Mo = mono_args(ctx, L, g, rs::mono_staged(int(L), C));
         Mo.src[0] = src;
         Mo.src_bstride[0] = g.orig_bstride;
         Mo.nsrc = 1;
@@ -497,7 +514,7 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
     A.fft_delta_step = n;
     const rs::RowMap src{orig, g.orig(), 0, uint32_t(N)}, dst{rec, g.rec(), 0, uint32_t(M)};
     if (use_mono(ctx, L, g, C)) {
-        rs::MonoArgs Mo = mono_args(ctx, L, g);
+        rs::MonoArgs Mo = mono_args(ctx, L, g, rs::mono_staged(int(L), C));
         Mo.src[0] = src;
         Mo.src_bstride[0] = g.orig_bstride;
         Mo.nsrc = 1;
@@ -667,7 +684,7 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
     }
     if (fused) {
         // one launch: every column workgroup evaluates eval_poly itself
-        rs::MonoArgs Mo = mono_args(ctx, u, g);
+        rs::MonoArgs Mo = mono_args(ctx, u, g, true, true);
         Mo.src[0] = rec_map;
         Mo.src_bstride[0] = g.rec_bstride;
         Mo.src[1] = orig_map;
@@ -727,7 +744,7 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
     rs::PassArgs A = base_args(ctx, g, nd);
     A.rowinfo = d_rowinfo;
     if (mono) {
-        rs::MonoArgs Mo = mono_args(ctx, u, g);
+        rs::MonoArgs Mo = mono_args(ctx, u, g, false);
         Mo.src[0] = rec_map;
         Mo.src[1] = orig_map;
         Mo.nsrc = 2;
@@ -971,6 +988,8 @@ rs_status rs_context_create(int device, rs_context **out) {
         check(hipMemcpy(ctx->d_tw, T.perm_by_skew.data(), T.perm_by_skew.size() * 4, hipMemcpyHostToDevice));
         check(hipMemcpy(ctx->d_lut, T.perm_by_log.data(), T.perm_by_log.size() * 4, hipMemcpyHostToDevice));
         check(hipMemcpy(ctx->d_lwfold, T.lw_fold.data(), T.lw_fold.size() * 2, hipMemcpyHostToDevice));
+        check(hipMalloc(&ctx->d_lut2, T.perm2_by_log.size() * 4));
+        check(hipMemcpy(ctx->d_lut2, T.perm2_by_log.data(), T.perm2_by_log.size() * 4, hipMemcpyHostToDevice));
         ctx->lw0 = T.log_walsh[0];
         const char *nm = getenv("RS_MI355X_NO_MONO");
         ctx->mono = !(nm && nm[0] == '1');
@@ -983,10 +1002,12 @@ rs_status rs_context_create(int device, rs_context **out) {
         const char *ma = getenv("RS_MI355X_MONO_ALL");
         ctx->mono_all = ma && ma[0] == '1';
         if (const char *mp = getenv("RS_MI355X_MONO_MAX_PACKS")) ctx->mono_max_packs = uint32_t(strtoul(mp, nullptr, 10));
+        if (const char *e2 = getenv("RS_MI355X_E2_MAX_PACKS")) ctx->e2_max_packs = uint32_t(strtoul(e2, nullptr, 10));
         // column-kernel twiddle images of every transform size, built now: a lazy
         // build inside an asynchronous call would stall the device with a
         // synchronous upload the first time a size is seen
         for (uint32_t L = kMonoMinL; L <= kMonoMaxL; ++L) mono_images(ctx, L);
+        for (uint32_t L = kMonoMinL; L <= 11; ++L) mono_images(ctx, L, 2);
         return RS_OK;
     });
     if (st != RS_OK) {
@@ -1002,6 +1023,9 @@ void rs_context_destroy(rs_context *ctx) {
     delete ctx->pipe;
     if (ctx->d_tw) (void)hipFree(ctx->d_tw);
     if (ctx->d_lut) (void)hipFree(ctx->d_lut);
+    if (ctx->d_lut2) (void)hipFree(ctx->d_lut2);
+    for (uint32_t *p : ctx->d_img2)
+        if (p) (void)hipFree(p);
     if (ctx->d_lwfold) (void)hipFree(ctx->d_lwfold);
     for (uint32_t *p : ctx->d_img)
         if (p) (void)hipFree(p);
@@ -1712,6 +1736,9 @@ rs_status rs_mono_enable(rs_context *ctx, int enable) {
     ctx->mono = (enable & 3) != 0;
     ctx->mono_all = (enable & 3) == 2;
     ctx->split = !(enable & 4);
+    // + 8: 4-element packs only; + 16: 2-element packs wherever the staged kernel runs
+    ctx->e2_max_packs = (enable & 8) ? 0u : (enable & 16) ? 0xFFFFFFFFu : 192u;
+    ctx->e2_encode = (enable & 16) != 0;
     return RS_OK;
 }
 

@@ -41,6 +41,29 @@ __host__ __device__ inline PackIO pack_io(const ShardFormat &f, uint32_t pk) {
     const uint32_t p = pk - f.full_packs, e = 4u * p;
     return {(f.full_packs >> 3) * 64u + e, f.tail_h, f.tail_h > e + 4u ? 4u : f.tail_h - e, true};
 }
+// 2-element packs (column kernel, E = 2): pack pk holds elements 2pk, 2pk + 1 of
+// a block (low bytes at 2 * (pk % 16), high bytes 32 further); tail packs as above
+// with 2 elements (shards.rs:38-74).
+__host__ __device__ inline PackIO pack_io2(const ShardFormat &f, uint32_t pk) {
+    const uint32_t full = f.full_packs == 0xFFFFFFFFu ? 0xFFFFFFFFu : f.full_packs * 2u;
+    if (pk < full) return {(pk >> 4) * 64u + (pk & 15u) * 2u, 32u, 2u, f.io_bytes != 0};
+    const uint32_t e = 2u * (pk - full);
+    return {(full >> 4) * 64u + e, f.tail_h, f.tail_h > e + 2u ? 2u : f.tail_h - e, true};
+}
+__device__ __forceinline__ uint32_t ld_half(const uint8_t *p, const PackIO &io) {
+    if (!io.bytes) return *reinterpret_cast<const uint16_t *>(p);
+    uint32_t v = p[0];
+    if (io.cnt > 1) v |= uint32_t(p[1]) << 8;
+    return v;
+}
+__device__ __forceinline__ void st_half(uint8_t *p, uint32_t v, const PackIO &io) {
+    if (!io.bytes) {
+        *reinterpret_cast<uint16_t *>(p) = uint16_t(v);
+        return;
+    }
+    p[0] = uint8_t(v);
+    if (io.cnt > 1) p[1] = uint8_t(v >> 8);
+}
 __device__ __forceinline__ uint32_t ld_word(const uint8_t *p, const PackIO &io) {
     if (!io.bytes) return *reinterpret_cast<const uint32_t *>(p);
     uint32_t v = 0;
@@ -140,18 +163,19 @@ char *launch_name_buf();
 enum MonoMode { kMonoEncodeHigh = 0, kMonoEncodeLow = 1, kMonoDecode = 2 };
 constexpr uint32_t kMonoFusedRows = 2048;  // largest work size of the fused-eval_poly decode
 struct MonoArgs {
-    uint32_t packs = 0;          // packs per row (shard_bytes / 8, rounded up)
+    uint32_t packs = 0;          // packs per row (shard_bytes / (2 * elems), rounded up)
     uint32_t packs_per_xcd = 0;  // ceil(packs / 8): workgroup b runs pack (b % 8) * packs_per_xcd + b / 8
     RowMap src[2];               // transform rows to load (others are zero)
     uint32_t nsrc = 0;
     RowMap dst;                  // transform rows to store (decode: erased originals only)
     uint32_t chunks = 1;         // high: IFFT chunks XOR-folded; low: FFT output chunks
     const uint32_t *img = nullptr;  // twiddle images of this L, image t at img + t * img_words
-    uint64_t img_words = 0;         // (n - 1) * 20
+    uint64_t img_words = 0;         // (n - 1) * table words (20, or 16 in the 2-element format)
+    uint32_t elems = 4;             // pack format: 4 or 2 elements per pack (rs_mono.hip Fmt)
     uint32_t ifft_img = 0, ifft_img_step = 0;  // image of IFFT chunk c: ifft_img + c * ifft_img_step
     uint32_t fft_img = 0, fft_img_step = 0;
     const uint32_t *rowinfo = nullptr;  // decode: bits 0-15 log factor, bit 16 erased
-    const uint32_t *lut = nullptr;      // perm tables by log factor (Engine::mul semantics)
+    const uint32_t *lut = nullptr;      // perm tables by log factor (Engine::mul semantics; format of elems)
     // decode with eval_poly fused into the staged kernel (every workgroup
     // evaluates it; no rowinfo): erased / received bits of the 2^L work rows,
     // as in EvalArgs

@@ -41,14 +41,19 @@ __device__ __forceinline__ void gf_muladd4(uint32_t &acc_l, uint32_t &acc_h, uin
     const uint32_t h0 = xh & 0x07070707u;
     const uint32_t h1 = uint32_t(x3 >> 32) & 0x07070707u;
     const uint32_t h2 = uint32_t(x6 >> 32) & 0x03030303u;
-    // low output plane: words 0-4 (from low byte), 10-14 (from high byte)
-    uint32_t pl = xor3(acc_l, __builtin_amdgcn_perm(t[1], t[0], l0), __builtin_amdgcn_perm(t[3], t[2], l1));
-    pl = xor3(pl, __builtin_amdgcn_perm(t[4], t[4], l2), __builtin_amdgcn_perm(t[11], t[10], h0));
-    acc_l = xor3(pl, __builtin_amdgcn_perm(t[13], t[12], h1), __builtin_amdgcn_perm(t[14], t[14], h2));
+    // low output plane: words 0-4 (from low byte), 10-14 (from high byte); the
+    // XOR tree is two levels deep (the butterflies of a layer are latency-bound)
+    const uint32_t la = xor3(__builtin_amdgcn_perm(t[1], t[0], l0), __builtin_amdgcn_perm(t[3], t[2], l1),
+                             __builtin_amdgcn_perm(t[4], t[4], l2));
+    const uint32_t lb = xor3(__builtin_amdgcn_perm(t[11], t[10], h0), __builtin_amdgcn_perm(t[13], t[12], h1),
+                             __builtin_amdgcn_perm(t[14], t[14], h2));
+    acc_l = xor3(acc_l, la, lb);
     // high output plane: words 5-9, 15-19
-    uint32_t ph = xor3(acc_h, __builtin_amdgcn_perm(t[6], t[5], l0), __builtin_amdgcn_perm(t[8], t[7], l1));
-    ph = xor3(ph, __builtin_amdgcn_perm(t[9], t[9], l2), __builtin_amdgcn_perm(t[16], t[15], h0));
-    acc_h = xor3(ph, __builtin_amdgcn_perm(t[18], t[17], h1), __builtin_amdgcn_perm(t[19], t[19], h2));
+    const uint32_t ha = xor3(__builtin_amdgcn_perm(t[6], t[5], l0), __builtin_amdgcn_perm(t[8], t[7], l1),
+                             __builtin_amdgcn_perm(t[9], t[9], l2));
+    const uint32_t hb = xor3(__builtin_amdgcn_perm(t[16], t[15], h0), __builtin_amdgcn_perm(t[18], t[17], h1),
+                             __builtin_amdgcn_perm(t[19], t[19], h2));
+    acc_h = xor3(acc_h, ha, hb);
 }
 
 __device__ __forceinline__ void gf_mul4(uint32_t &xl, uint32_t &xh, const uint32_t *__restrict__ t) {
@@ -56,6 +61,51 @@ __device__ __forceinline__ void gf_mul4(uint32_t &xl, uint32_t &xh, const uint32
     gf_muladd4(l, h, xl, xh, t);
     xl = l;
     xh = h;
+}
+
+// 2-element format (gf_tables.cpp fill_perm2): x = [lo0 lo1 hi0 hi1], t = 16
+// words.  Per 2-bit field f: a "direct" lookup on the field values in place
+// (low-byte fields -> low output bytes, high-byte fields -> high output bytes)
+// and a "cross" lookup on the word rotated by 16 bits (high-byte fields -> low
+// output bytes and vice versa); selectors of the high half index the table's
+// upper 4 bytes (+4).  12 field ops, 8 v_perm, 4 v_bitop3 XOR3 per 2 elements.
+__device__ __forceinline__ void gf_muladd2(uint32_t &acc, uint32_t x, const uint32_t *__restrict__ t) {
+    const uint32_t xr = __builtin_amdgcn_alignbit(x, x, 16);
+    const uint64_t xx = (uint64_t(xr) << 32) | x;
+    uint64_t x2, x4, x6;
+    asm("v_lshrrev_b64 %0, 2, %1" : "=v"(x2) : "v"(xx));
+    asm("v_lshrrev_b64 %0, 4, %1" : "=v"(x4) : "v"(xx));
+    asm("v_lshrrev_b64 %0, 6, %1" : "=v"(x6) : "v"(xx));
+    // (v & M) | C in one v_bitop3 (truth table 0xEA = S0 & S1 | S2): VOP3 takes no
+    // literal, so the compiler keeps M and C in registers
+    constexpr uint32_t M = 0x03030303u, C = 0x04040000u;
+    auto sel = [](uint32_t v) { return __builtin_amdgcn_bitop3_b32(v, M, C, 0xEA); };
+    const uint32_t d0 = sel(x), c0 = sel(xr);
+    const uint32_t d1 = sel(uint32_t(x2)), c1 = sel(uint32_t(x2 >> 32));
+    const uint32_t d2 = sel(uint32_t(x4)), c2 = sel(uint32_t(x4 >> 32));
+    const uint32_t d3 = sel(uint32_t(x6)), c3 = sel(uint32_t(x6 >> 32));
+    const uint32_t a = xor3(__builtin_amdgcn_perm(t[1], t[0], d0), __builtin_amdgcn_perm(t[3], t[2], c0),
+                            __builtin_amdgcn_perm(t[5], t[4], d1));
+    const uint32_t b = xor3(__builtin_amdgcn_perm(t[7], t[6], c1), __builtin_amdgcn_perm(t[9], t[8], d2),
+                            __builtin_amdgcn_perm(t[11], t[10], c2));
+    const uint32_t c = xor3(acc, __builtin_amdgcn_perm(t[13], t[12], d3), __builtin_amdgcn_perm(t[15], t[14], c3));
+    acc = xor3(a, b, c);
+}
+
+__device__ __forceinline__ void gf_mul2(uint32_t &x, const uint32_t *__restrict__ t) {
+    uint32_t acc = 0;
+    gf_muladd2(acc, x, t);
+    x = acc;
+}
+
+__device__ __forceinline__ void ifft_bfly2(uint32_t &a, uint32_t &b, const uint32_t *__restrict__ t) {
+    b ^= a;
+    gf_muladd2(a, b, t);
+}
+
+__device__ __forceinline__ void fft_bfly2(uint32_t &a, uint32_t &b, const uint32_t *__restrict__ t) {
+    gf_muladd2(a, b, t);
+    b ^= a;
 }
 
 // IFFT butterfly (engine_naive.rs:96-100): b ^= a; a ^= b * m

@@ -290,11 +290,24 @@ __device__ __forceinline__ void xpose(uint32_t &a, uint32_t &b, uint32_t lane) {
     }
 }
 
-template <int L, int LR>
+// Pack format: E = 4 elements per pack (a row is a low-byte word and a
+// high-byte word, 20-word tables, rs_gf.hpp gf_muladd4) or E = 2 (a row is one
+// word [lo0 lo1 hi0 hi1], 16-word tables, gf_muladd2): the 2-element form gives
+// a shard matrix twice the workgroups (packs = shard_bytes / 4), for matrices
+// whose 4-element packs leave CUs idle.
+template <int E>
+struct Fmt {
+    static_assert(E == 4 || E == 2, "pack format");
+    static constexpr int kTW = E == 4 ? 20 : 16;  // table words
+    static constexpr uint32_t kPC = kTW / 4;      // 16-byte pieces per table
+    static constexpr bool kHi = E == 4;           // rows have a separate high-byte word
+};
+
+template <int L, int LR, int E = 4>
 struct Col {
     static constexpr int R = 1 << LR;
     static constexpr uint32_t n = 1u << L;
-    uint32_t lo[R], hi[R];
+    uint32_t lo[R], hi[E == 4 ? R : 1];
 };
 
 // Index of register pair (i, i | 2^s) among the pairs of register bit s.
@@ -325,8 +338,10 @@ struct GlobalTabs {
     }
 };
 
-template <int L, int LR, bool SPLIT = false>
+template <int L, int LR, bool SPLIT = false, int E = 4>
 struct Stage {
+    static constexpr int TW = Fmt<E>::kTW;
+    static constexpr uint32_t PC = Fmt<E>::kPC;
     static constexpr int IW = LR + 6, WB = L - IW - (SPLIT ? 1 : 0);
     static constexpr uint32_t n = 1u << L, W = 1u << IW;
     // layers of the last (FFT) in-wave phase
@@ -347,14 +362,14 @@ struct Stage {
     static constexpr uint32_t kShF = WB > 0 ? (n >> WB) - 1 : 0;     // shared: FFT layers WB..L-1
     static constexpr uint32_t kShared = kShI + kShF;
     static constexpr uint32_t kWaves = 1u << (L - LR - 6);
-    static constexpr uint32_t plane_words = 2 * n;
-    static constexpr uint32_t words = plane_words + (kShared + kWaves * kPriv) * 20;
+    static constexpr uint32_t plane_words = (E == 4 ? 2 : 1) * n;
+    static constexpr uint32_t words = plane_words + (kShared + kWaves * kPriv) * TW;
     // encode (IFFT and FFT on different skew offsets t_i, t_f): phase 3's tables
     // are phase 1's XOR D_b, one table per phase-3 layer b (twiddles are
     // GF(2)-linear in the global group index, so are the perm tables:
     // D_b = the table of group (t_i ^ t_f) * n / 2^(b+1)), kept after the shared tables
     static constexpr uint32_t kD = NB3;
-    static constexpr uint32_t words_enc = words + kD * 20;
+    static constexpr uint32_t words_enc = words + kD * TW;
     static constexpr uint32_t words_dec = words + n;  // + per-row decode info (fused eval_poly)
     // SPLIT decode: + a second column plane (the cross-half step's formal-derivative values)
     static constexpr uint32_t words_split = words_dec + (SPLIT ? plane_words : 0);
@@ -366,12 +381,12 @@ struct Stage {
 // wave-private region: a wave's rows there are 2^IW consecutive rows, so its
 // groups are its own.  Phase 2 (top bits in-wave, wave bits low) reads the
 // region shared by all waves.
-template <int L, int LR, bool SPLIT = false>
+template <int L, int LR, bool SPLIT = false, int E = 4>
 struct LdsTabs {
-    using G = Stage<L, LR, SPLIT>;
+    using G = Stage<L, LR, SPLIT, E>;
     const uint32_t *priv, *shared, *img_i, *img_f;
     template <int, int, typename S, int I, int PH>
-    __device__ __forceinline__ void get(int x, uint32_t row, uint32_t (&t)[20]) const {
+    __device__ __forceinline__ void get(int x, uint32_t row, uint32_t (&t)[Fmt<E>::kTW]) const {
         uint32_t slot;
         const uint32_t *base;
         if constexpr ((PH == 1 || PH == 3) && G::B0 == 1 && S::v.ops[I].bit == 0) {
@@ -388,12 +403,12 @@ struct LdsTabs {
             base = shared;
         }
 #ifdef RS_MONO_FAKE_TABS  // tools/mono_probe.hip: tables without LDS traffic
-        for (int q = 0; q < 20; ++q) t[q] = slot * 0x01010101u + q + uint32_t(reinterpret_cast<uintptr_t>(base));
+        for (int q = 0; q < G::TW; ++q) t[q] = slot * 0x01010101u + q + uint32_t(reinterpret_cast<uintptr_t>(base));
         return;
 #endif
-        const uint4 *p = reinterpret_cast<const uint4 *>(base) + slot * 5u;
+        const uint4 *p = reinterpret_cast<const uint4 *>(base) + slot * G::PC;
 #pragma unroll
-        for (int q = 0; q < 5; ++q) {
+        for (int q = 0; q < int(G::PC); ++q) {
             const uint4 v = p[q];
             t[4 * q] = v.x, t[4 * q + 1] = v.y, t[4 * q + 2] = v.z, t[4 * q + 3] = v.w;
         }
@@ -415,9 +430,9 @@ constexpr int phase_of() {
     else return I < ri ? 1 : 2;
 }
 
-template <int L, int LR, typename S, int I, bool FFT, typename TS>
+template <int L, int LR, typename S, int I, bool FFT, typename TS, int TW>
 __device__ __forceinline__ void load_layer_tabs(const TS &ts, uint32_t lane, uint32_t wave,
-                                                uint32_t (&t)[(1 << LR) / 2][20]) {
+                                                uint32_t (&t)[(1 << LR) / 2][TW]) {
     constexpr Op op = S::v.ops[I];
     const uint32_t lr = lane_rows<S, I>(lane, wave);
     static_for<0, (1 << LR)>([&](auto ic) {
@@ -428,35 +443,40 @@ __device__ __forceinline__ void load_layer_tabs(const TS &ts, uint32_t lane, uin
     });
 }
 
-template <int L, int LR, typename S, int I, bool IFFT>
-__device__ __forceinline__ void apply_layer(const uint32_t (&t)[(1 << LR) / 2][20], Col<L, LR> &c) {
+template <int L, int LR, typename S, int I, bool IFFT, int E>
+__device__ __forceinline__ void apply_layer(const uint32_t (&t)[(1 << LR) / 2][Fmt<E>::kTW], Col<L, LR, E> &c) {
     constexpr Op op = S::v.ops[I];
     static_for<0, (1 << LR)>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         constexpr int i2 = i | (1 << op.rs);
         if constexpr (!((i >> op.rs) & 1)) {
-            if constexpr (IFFT) ifft_bfly(c.lo[i], c.hi[i], c.lo[i2], c.hi[i2], t[pair_of(i, op.rs)]);
-            else fft_bfly(c.lo[i], c.hi[i], c.lo[i2], c.hi[i2], t[pair_of(i, op.rs)]);
+            if constexpr (E == 2) {
+                if constexpr (IFFT) ifft_bfly2(c.lo[i], c.lo[i2], t[pair_of(i, op.rs)]);
+                else fft_bfly2(c.lo[i], c.lo[i2], t[pair_of(i, op.rs)]);
+            } else {
+                if constexpr (IFFT) ifft_bfly(c.lo[i], c.hi[i], c.lo[i2], c.hi[i2], t[pair_of(i, op.rs)]);
+                else fft_bfly(c.lo[i], c.hi[i], c.lo[i2], c.hi[i2], t[pair_of(i, op.rs)]);
+            }
         }
     });
 }
 
-template <int L, int LR, typename S, int I>
-__device__ __forceinline__ void apply_xpose(Col<L, LR> &c, uint32_t lane) {
+template <int L, int LR, typename S, int I, int E>
+__device__ __forceinline__ void apply_xpose(Col<L, LR, E> &c, uint32_t lane) {
     constexpr Op op = S::v.ops[I];
     static_for<0, (1 << LR)>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         constexpr int i2 = i | (1 << op.rs);
         if constexpr (!((i >> op.rs) & 1)) {
             xpose<op.ls>(c.lo[i], c.lo[i2], lane);
-            xpose<op.ls>(c.hi[i], c.hi[i2], lane);
+            if constexpr (Fmt<E>::kHi) xpose<op.ls>(c.hi[i], c.hi[i2], lane);
         }
     });
 }
 
 // Whole-column exchange through LDS from placement maps[I] to maps[I + 1].
-template <int L, int LR, typename S, int I>
-__device__ __forceinline__ void apply_remap(Col<L, LR> &c, uint32_t *plane, uint32_t lane, uint32_t wave) {
+template <int L, int LR, typename S, int I, int E>
+__device__ __forceinline__ void apply_remap(Col<L, LR, E> &c, uint32_t *plane, uint32_t lane, uint32_t wave) {
     constexpr uint32_t n = 1u << L;
     __syncthreads();
     const uint32_t a = lane_rows<S, I>(lane, wave);
@@ -464,7 +484,7 @@ __device__ __forceinline__ void apply_remap(Col<L, LR> &c, uint32_t *plane, uint
         constexpr int i = decltype(ic)::value;
         const uint32_t x = swz<L>(a | reg_rows<S, I, LR>(i));
         plane[x] = c.lo[i];
-        plane[n + x] = c.hi[i];
+        if constexpr (Fmt<E>::kHi) plane[n + x] = c.hi[i];
     });
     __syncthreads();
     const uint32_t b = lane_rows<S, I + 1>(lane, wave);
@@ -472,7 +492,7 @@ __device__ __forceinline__ void apply_remap(Col<L, LR> &c, uint32_t *plane, uint
         constexpr int i = decltype(ic)::value;
         const uint32_t x = swz<L>(b | reg_rows<S, I + 1, LR>(i));
         c.lo[i] = plane[x];
-        c.hi[i] = plane[n + x];
+        if constexpr (Fmt<E>::kHi) c.hi[i] = plane[n + x];
     });
 }
 
@@ -503,8 +523,8 @@ struct NoHook {
 // wave with `pre` false skips the ops before the remap, with `alive` false
 // the ops after it.
 template <int L, int LR, bool FFT, int B0, int KHOOK = -1, bool SPLIT = false, typename TS, typename PreRemap,
-          typename Hook = NoHook>
-__device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR> &c, uint32_t *plane, uint32_t lane, uint32_t wave,
+          int E, typename Hook = NoHook>
+__device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR, E> &c, uint32_t *plane, uint32_t lane, uint32_t wave,
                                         const PreRemap &pre_remap, bool alive = true, bool pre = true,
                                         const Hook &hook = Hook{}) {
     using S = SeqOf<L, LR, FFT, SPLIT>;
@@ -513,7 +533,7 @@ __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR> &c, uint32_t *p
     constexpr int RI = remap_index(S::v);
     constexpr int NL1 = layer_ordinal(S::v, RI);  // layers before the remap
     constexpr int B = B0 < NL ? B0 : NL;
-    uint32_t tb[B][NT][20];
+    uint32_t tb[B][NT][Fmt<E>::kTW];
     auto request = [&](auto kc) {
         constexpr int k = decltype(kc)::value;
         if constexpr (k == KHOOK) hook();
@@ -530,20 +550,20 @@ __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR> &c, uint32_t *p
         constexpr Op op = S::v.ops[I];
         if constexpr (op.kind == kOpXpose) {
 #ifndef RS_MONO_SKIP_XPOSE  // tools/mono_probe.hip ablation
-            apply_xpose<L, LR, S, I>(c, lane);
+            apply_xpose<L, LR, S, I, E>(c, lane);
 #endif
         } else if constexpr (op.kind == kOpRemap) {
             pre_remap();
             RS_MSTAMP(FFT ? 8 : 3);
 #ifndef RS_MONO_SKIP_REMAP  // tools/mono_probe.hip ablation
-            apply_remap<L, LR, S, I>(c, plane, lane, wave);
+            apply_remap<L, LR, S, I, E>(c, plane, lane, wave);
 #endif
             RS_MSTAMP(FFT ? 9 : 4);
             if (alive) prime(std::integral_constant<int, NL1>{}, std::integral_constant<int, NL>{});
         } else {
             constexpr int k = layer_ordinal(S::v, I);
 #ifndef RS_MONO_SKIP_LAYERS
-            apply_layer<L, LR, S, I, !FFT>(tb[k % B], c);
+            apply_layer<L, LR, S, I, !FFT, E>(tb[k % B], c);
 #endif
             constexpr int end = k < NL1 ? NL1 : NL;
             if constexpr (k + B < end) {
@@ -605,7 +625,8 @@ __device__ __forceinline__ uint32_t paired_row(uint32_t lane, uint32_t wave, int
 // Load transform rows `chunk * n + row` (placement: start of the IFFT) as
 // paired words; finish_col completes them.  Missing rows inside the caller's
 // matrices are read and discarded by the decode's scaling.
-template <int L, int LR, bool SPLIT = false>
+// (2-element packs: the paired words are the 16-bit low and high halves)
+template <int L, int LR, bool SPLIT = false, int E = 4>
 __device__ __forceinline__ void issue_col(const MonoArgs &A, uint32_t chunk, const PackIO &io, const StripeBases &sb,
                                           uint32_t (&w)[2 << LR], uint32_t lane, uint32_t wave, bool live = true) {
     using S = SeqOf<L, LR, false, SPLIT>;
@@ -620,7 +641,7 @@ __device__ __forceinline__ void issue_col(const MonoArgs &A, uint32_t chunk, con
         p = nullptr;
         v = r * 0x9E3779B9u + off;
 #endif
-        if (p && live) v = ld_word(p + off, io);
+        if (p && live) v = E == 4 ? ld_word(p + off, io) : ld_half(p + off, io);
         w[j] = v;
     });
 }
@@ -628,14 +649,15 @@ __device__ __forceinline__ void issue_col(const MonoArgs &A, uint32_t chunk, con
 // Decode scaling (rate_high.rs:213-231): received rows are multiplied by
 // exp(log factor), erased rows become zero; rowinfo is indexed by work row.
 // scale_issue requests the multiply tables, finish_col applies them.
-template <int L, int LR>
+template <int L, int LR, int E = 4>
 struct ScaleTabs {
-    uint32_t t[1 << LR][20];
+    uint32_t t[1 << LR][Fmt<E>::kTW];
     uint32_t erased;  // bit i: register i's row is not received
 };
-template <int L, int LR, bool SPLIT = false>
-__device__ __forceinline__ void scale_issue(const MonoArgs &A, const uint32_t *rowinfo, ScaleTabs<L, LR> &st,
+template <int L, int LR, bool SPLIT = false, int E = 4>
+__device__ __forceinline__ void scale_issue(const MonoArgs &A, const uint32_t *rowinfo, ScaleTabs<L, LR, E> &st,
                                             uint32_t lane, uint32_t wave) {
+    constexpr uint32_t PC = Fmt<E>::kPC;
     using S = SeqOf<L, LR, false, SPLIT>;
     const uint32_t a = lane_rows<S, 0>(lane, wave);
     st.erased = 0;
@@ -649,27 +671,35 @@ __device__ __forceinline__ void scale_issue(const MonoArgs &A, const uint32_t *r
         lg = 0;
 #endif
         st.erased |= ((f >> 16) & 1u) << i;
-        const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + lg * 5u;
+        const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + lg * PC;
 #pragma unroll
-        for (int v = 0; v < 5; ++v) {
+        for (int v = 0; v < int(PC); ++v) {
             const uint4 x = q[v];
             st.t[i][4 * v] = x.x, st.t[i][4 * v + 1] = x.y, st.t[i][4 * v + 2] = x.z, st.t[i][4 * v + 3] = x.w;
         }
     });
 }
 
-template <int L, int LR, bool SCALE>
-__device__ __forceinline__ void finish_col(uint32_t (&w)[2 << LR], const ScaleTabs<L, LR> *st, Col<L, LR> &c,
+template <int L, int LR, bool SCALE, int E>
+__device__ __forceinline__ void finish_col(uint32_t (&w)[2 << LR], const ScaleTabs<L, LR, E> *st, Col<L, LR, E> &c,
                                            uint32_t lane) {
     constexpr int R = 1 << LR;
     static_for<0, R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         xpose<0>(w[2 * i], w[2 * i + 1], lane);
-        c.lo[i] = w[2 * i];
-        c.hi[i] = w[2 * i + 1];
-        if constexpr (SCALE) {
-            gf_mul4(c.lo[i], c.hi[i], st->t[i]);
-            if ((st->erased >> i) & 1u) c.lo[i] = c.hi[i] = 0;
+        if constexpr (E == 2) {
+            c.lo[i] = w[2 * i] | (w[2 * i + 1] << 16);
+            if constexpr (SCALE) {
+                gf_mul2(c.lo[i], st->t[i]);
+                if ((st->erased >> i) & 1u) c.lo[i] = 0;
+            }
+        } else {
+            c.lo[i] = w[2 * i];
+            c.hi[i] = w[2 * i + 1];
+            if constexpr (SCALE) {
+                gf_mul4(c.lo[i], c.hi[i], st->t[i]);
+                if ((st->erased >> i) & 1u) c.lo[i] = c.hi[i] = 0;
+            }
         }
     });
 }
@@ -681,17 +711,18 @@ __device__ __forceinline__ void load_col(const MonoArgs &A, uint32_t chunk, cons
     issue_col<L, LR>(A, chunk, io, sb, w, lane, wave);
     ScaleTabs<L, LR> st;
     if constexpr (SCALE) scale_issue<L, LR>(A, A.rowinfo, st, lane, wave);
-    finish_col<L, LR, SCALE>(w, &st, c, lane);
+    finish_col<L, LR, SCALE, 4>(w, &st, c, lane);
 }
 
 // Store transform rows `chunk * n + row` that fall in A.dst (placement: end
 // of the FFT), paired like the loads.  REVEAL (decode): only erased rows,
 // multiplied by exp(65535 - log factor) (rate_high.rs:241-245).
-template <int L, int LR, bool REVEAL, bool SPLIT = false>
+template <int L, int LR, bool REVEAL, bool SPLIT = false, int E = 4>
 __device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *rowinfo, uint32_t chunk,
-                                          const PackIO &io, const StripeBases &sb, Col<L, LR> &c, uint32_t lane,
+                                          const PackIO &io, const StripeBases &sb, Col<L, LR, E> &c, uint32_t lane,
                                           uint32_t wave) {
     using S = SeqOf<L, LR, true, SPLIT>;
+    constexpr uint32_t PC = Fmt<E>::kPC;
     constexpr int I = S::v.count;
     constexpr int R = 1 << LR;
     const uint32_t base = chunk * (1u << L);
@@ -705,21 +736,27 @@ __device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *row
             // shared dummy table (log 0), so their gathers cost no cache lines
             const bool need = (f & 0x10000u) && r >= A.dst.row_begin && r < A.dst.row_end;
             const uint32_t lg = need ? 65535u - (f & 0xFFFFu) : 0u;
-            uint32_t t[20];
-            const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + lg * 5u;
+            uint32_t t[Fmt<E>::kTW];
+            const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + lg * PC;
 #pragma unroll
-            for (int v = 0; v < 5; ++v) {
+            for (int v = 0; v < int(PC); ++v) {
                 const uint4 x = q[v];
                 t[4 * v] = x.x, t[4 * v + 1] = x.y, t[4 * v + 2] = x.z, t[4 * v + 3] = x.w;
             }
-            gf_mul4(c.lo[i], c.hi[i], t);
+            if constexpr (E == 2) gf_mul2(c.lo[i], t);
+            else gf_mul4(c.lo[i], c.hi[i], t);
         });
     }
     uint32_t w[2 * R];
     static_for<0, R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        w[2 * i] = c.lo[i];
-        w[2 * i + 1] = c.hi[i];
+        if constexpr (E == 2) {
+            w[2 * i] = c.lo[i] & 0xFFFFu;
+            w[2 * i + 1] = c.lo[i] >> 16;
+        } else {
+            w[2 * i] = c.lo[i];
+            w[2 * i + 1] = c.hi[i];
+        }
         xpose<0>(w[2 * i], w[2 * i + 1], lane);
     });
     const uint32_t off = io.lo + ((lane & 1u) ? io.hi_delta : 0u);
@@ -734,7 +771,8 @@ __device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *row
 #endif
             if (keep) {
                 uint8_t *p = sb.dst + uint64_t(r - A.dst.row_begin) * A.dst.stride;
-                st_word(p + off, w[j], io);
+                if constexpr (E == 2) st_half(p + off, w[j], io);
+                else st_word(p + off, w[j], io);
             }
         }
     });
@@ -745,8 +783,9 @@ __device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *row
 // Terms on register bits come from the lane's own registers, terms on lane
 // bits from the partner lane (DPP / permlane), terms on wave bits through the
 // LDS plane -- read only by the waves whose wave bit is clear.
-template <int L, int LR>
-__device__ __forceinline__ void formal_derivative(Col<L, LR> &c, uint32_t *plane, uint32_t lane, uint32_t wave) {
+template <int L, int LR, int E>
+__device__ __forceinline__ void formal_derivative(Col<L, LR, E> &c, uint32_t *plane, uint32_t lane, uint32_t wave) {
+    constexpr bool HI = Fmt<E>::kHi;
     using S = SeqOf<L, LR, true>;
     constexpr uint32_t n = 1u << L;
     constexpr int R = 1 << LR;
@@ -759,19 +798,19 @@ __device__ __forceinline__ void formal_derivative(Col<L, LR> &c, uint32_t *plane
             constexpr int i = decltype(ic)::value;
             const uint32_t x = swz<L>(a | reg_rows<S, 0, LR>(i));
             plane[x] = c.lo[i];
-            plane[n + x] = c.hi[i];
+            if constexpr (HI) plane[n + x] = c.hi[i];
         });
     }
-    uint32_t l[R], h[R];
+    uint32_t l[R], h[HI ? R : 1];
     static_for<0, R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         l[i] = c.lo[i];
-        h[i] = c.hi[i];
+        if constexpr (HI) h[i] = c.hi[i];
         static_for<0, LR>([&](auto sc) {  // register bits
             constexpr int sb = decltype(sc)::value;
             if constexpr (!((i >> sb) & 1)) {
                 l[i] ^= c.lo[i | (1 << sb)];
-                h[i] ^= c.hi[i | (1 << sb)];
+                if constexpr (HI) h[i] ^= c.hi[i | (1 << sb)];
             }
         });
     });
@@ -781,7 +820,7 @@ __device__ __forceinline__ void formal_derivative(Col<L, LR> &c, uint32_t *plane
         static_for<0, R>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             l[i] ^= lane_xor<J>(c.lo[i], lane) & keep;
-            h[i] ^= lane_xor<J>(c.hi[i], lane) & keep;
+            if constexpr (HI) h[i] ^= lane_xor<J>(c.hi[i], lane) & keep;
         });
     });
     if constexpr (kWaves) {
@@ -794,7 +833,7 @@ __device__ __forceinline__ void formal_derivative(Col<L, LR> &c, uint32_t *plane
                         constexpr int i = decltype(ic)::value;
                         const uint32_t x = swz<L>((a | reg_rows<S, 0, LR>(i)) ^ (1u << m.wave[k]));
                         l[i] ^= plane[x];
-                        h[i] ^= plane[n + x];
+                        if constexpr (HI) h[i] ^= plane[n + x];
                     });
                 }
             }
@@ -803,26 +842,26 @@ __device__ __forceinline__ void formal_derivative(Col<L, LR> &c, uint32_t *plane
     static_for<0, R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         c.lo[i] = l[i];
-        c.hi[i] = h[i];
+        if constexpr (HI) c.hi[i] = h[i];
     });
 }
 
 // In-wave terms of the formal derivative (register and lane bits) of the
 // values v under placement m: out = v ^ XOR over those bits b with q_b = 0 of
 // v[q | 2^b] (src/engine/utils.rs:99-104, closed form).
-template <int LR, typename S>
+template <int LR, typename S, bool HI = true>
 __device__ __forceinline__ void fd_in_wave(const uint32_t (&vl)[1 << LR], const uint32_t (&vh)[1 << LR],
                                            uint32_t (&l)[1 << LR], uint32_t (&h)[1 << LR], uint32_t lane) {
     constexpr int R = 1 << LR;
     static_for<0, R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         l[i] = vl[i];
-        h[i] = vh[i];
+        if constexpr (HI) h[i] = vh[i];
         static_for<0, LR>([&](auto sc) {
             constexpr int sb = decltype(sc)::value;
             if constexpr (!((i >> sb) & 1)) {
                 l[i] ^= vl[i | (1 << sb)];
-                h[i] ^= vh[i | (1 << sb)];
+                if constexpr (HI) h[i] ^= vh[i | (1 << sb)];
             }
         });
     });
@@ -832,7 +871,7 @@ __device__ __forceinline__ void fd_in_wave(const uint32_t (&vl)[1 << LR], const 
         static_for<0, R>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             l[i] ^= lane_xor<J>(vl[i], lane) & keep;
-            h[i] ^= lane_xor<J>(vh[i], lane) & keep;
+            if constexpr (HI) h[i] ^= lane_xor<J>(vh[i], lane) & keep;
         });
     });
 }
@@ -847,10 +886,12 @@ __device__ __forceinline__ void fd_in_wave(const uint32_t (&vl)[1 << LR], const 
 // with the FFT; they compute both halves' values of their row positions, so
 // the other half's waves only hand over their rows.  Three barriers; every
 // wave reaches them.
-template <int L, int LR>
-__device__ __forceinline__ void split_top(Col<L, LR> &c, uint32_t *plane, uint32_t *plane2, const uint32_t *tab_i,
+template <int L, int LR, int E>
+__device__ __forceinline__ void split_top(Col<L, LR, E> &c, uint32_t *plane, uint32_t *plane2, const uint32_t *tab_i,
                                           const uint32_t *tab_f, uint32_t lane, uint32_t wave, uint32_t out_half) {
     using S = SeqOf<L, LR, true, true>;
+    constexpr bool HI = Fmt<E>::kHi;
+    constexpr int TW = Fmt<E>::kTW;
     constexpr Map m = S::v.maps[0];
     constexpr int KT = L - 1 - (LR + 6);  // the wave bit holding the top row bit (the half)
     static_assert(m.wave[KT] == L - 1, "split placement: the top row bit is the highest wave bit");
@@ -863,15 +904,15 @@ __device__ __forceinline__ void split_top(Col<L, LR> &c, uint32_t *plane, uint32
         constexpr int i = decltype(ic)::value;
         const uint32_t x = swz<L>(a | reg_rows<S, 0, LR>(i));
         plane[x] = c.lo[i];
-        plane[n + x] = c.hi[i];
+        if constexpr (HI) plane[n + x] = c.hi[i];
     });
     __syncthreads();
     uint32_t ll[R], lh[R], ul[R], uh[R];  // lower / upper half values of the lane's row positions
-    uint32_t fl[R], fh[R], gl[R], gh[R];  // their in-wave derivative terms
-    uint32_t tf[20];
+    uint32_t fl[R], fh[R], gl[R], gh[R];  // their in-wave derivative terms (h: E = 4 only)
+    uint32_t tf[TW];
     if (out) {
-        uint32_t ti[20];
-        static_for<0, 5>([&](auto qc) {  // the top layers' tables: one each, wave-uniform
+        uint32_t ti[TW];
+        static_for<0, TW / 4>([&](auto qc) {  // the top layers' tables: one each, wave-uniform
             constexpr int q = decltype(qc)::value;
             const uint4 v = reinterpret_cast<const uint4 *>(tab_i)[q];
             ti[4 * q] = v.x, ti[4 * q + 1] = v.y, ti[4 * q + 2] = v.z, ti[4 * q + 3] = v.w;
@@ -881,21 +922,28 @@ __device__ __forceinline__ void split_top(Col<L, LR> &c, uint32_t *plane, uint32
         static_for<0, R>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             const uint32_t x = swz<L>((a | reg_rows<S, 0, LR>(i)) ^ H);
-            const uint32_t pl = plane[x], ph = plane[n + x];
+            const uint32_t pl = plane[x];
             ll[i] = out_half ? pl : c.lo[i];
-            lh[i] = out_half ? ph : c.hi[i];
             ul[i] = out_half ? c.lo[i] : pl;
-            uh[i] = out_half ? c.hi[i] : ph;
-            ifft_bfly(ll[i], lh[i], ul[i], uh[i], ti);
+            if constexpr (HI) {
+                const uint32_t ph = plane[n + x];
+                lh[i] = out_half ? ph : c.hi[i];
+                uh[i] = out_half ? c.hi[i] : ph;
+                ifft_bfly(ll[i], lh[i], ul[i], uh[i], ti);
+            } else {
+                ifft_bfly2(ll[i], ul[i], ti);
+            }
             // both halves' values, at their own rows, for the wave-bit terms
             const uint32_t y = swz<L>((a | reg_rows<S, 0, LR>(i)) & (H - 1));
             plane2[y] = ll[i];
-            plane2[n + y] = lh[i];
             plane2[y + H] = ul[i];  // (the upper value of position q sits at swz(q) + H)
-            plane2[n + y + H] = uh[i];
+            if constexpr (HI) {
+                plane2[n + y] = lh[i];
+                plane2[n + y + H] = uh[i];
+            }
         });
-        fd_in_wave<LR, S>(ll, lh, fl, fh, lane);
-        fd_in_wave<LR, S>(ul, uh, gl, gh, lane);
+        fd_in_wave<LR, S, HI>(ll, lh, fl, fh, lane);
+        fd_in_wave<LR, S, HI>(ul, uh, gl, gh, lane);
     }
     __syncthreads();
     if (out) {
@@ -908,9 +956,11 @@ __device__ __forceinline__ void split_top(Col<L, LR> &c, uint32_t *plane, uint32
                         const uint32_t q = ((a | reg_rows<S, 0, LR>(i)) & (H - 1)) ^ (1u << m.wave[k]);
                         const uint32_t x = swz<L>(q);
                         fl[i] ^= plane2[x];
-                        fh[i] ^= plane2[n + x];
                         gl[i] ^= plane2[x + H];
-                        gh[i] ^= plane2[n + x + H];
+                        if constexpr (HI) {
+                            fh[i] ^= plane2[n + x];
+                            gh[i] ^= plane2[n + x + H];
+                        }
                     });
                 }
             }
@@ -918,10 +968,14 @@ __device__ __forceinline__ void split_top(Col<L, LR> &c, uint32_t *plane, uint32
         static_for<0, R>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             fl[i] ^= ul[i];  // bit L-1 term: lower rows take their upper partner (pre-derivative)
-            fh[i] ^= uh[i];
-            fft_bfly(fl[i], fh[i], gl[i], gh[i], tf);
+            if constexpr (HI) {
+                fh[i] ^= uh[i];
+                fft_bfly(fl[i], fh[i], gl[i], gh[i], tf);
+                c.hi[i] = out_half ? gh[i] : fh[i];
+            } else {
+                fft_bfly2(fl[i], gl[i], tf);
+            }
             c.lo[i] = out_half ? gl[i] : fl[i];
-            c.hi[i] = out_half ? gh[i] : fh[i];
         });
     }
 }
@@ -1045,41 +1099,41 @@ __device__ __forceinline__ void col_eval_poly(const MonoArgs &A, uint32_t ebits,
 // LDS staging of the twiddle tables (STAGED kernel): 16-byte pieces q of the
 // wave-private region (phase 1 from the IFFT image, phase 3 from the FFT
 // image) and of the shared region.
-template <int L, int LR, bool SPLIT = false>
+template <int L, int LR, bool SPLIT, int E>
 __device__ __forceinline__ uint4 priv_piece(const uint32_t *img, uint32_t wave, uint32_t q) {
-    using G = Stage<L, LR, SPLIT>;
-    const uint32_t t = q / 5, piece = q - t * 5;
+    using G = Stage<L, LR, SPLIT, E>;
+    const uint32_t t = q / G::PC, piece = q - t * G::PC;
     const uint32_t y = (G::W >> G::B0) - t;                   // in [1, W >> B0]
     const int b = G::IW - int(32 - __builtin_clz(y - 1));    // IW - ceil(log2 y)
     const uint32_t local = t - ((G::W >> G::B0) - (G::W >> b));
     const uint32_t slot = G::n - (G::n >> b) + wave * (G::W >> (b + 1)) + local;
-    return reinterpret_cast<const uint4 *>(img)[slot * 5u + piece];
+    return reinterpret_cast<const uint4 *>(img)[slot * G::PC + piece];
 }
 // 16-byte piece q of the layer-0 tables of wave `wave`'s phase-1 / -3 rows
 // (image slots wave * W/2 .. : contiguous, one coalesced read per wave)
-template <int L, int LR, bool SPLIT = false>
+template <int L, int LR, bool SPLIT, int E>
 __device__ __forceinline__ uint4 l0_piece(const uint32_t *img, uint32_t wave, uint32_t q) {
-    using G = Stage<L, LR, SPLIT>;
-    return reinterpret_cast<const uint4 *>(img)[wave * G::kL0 * 5u + q];
+    using G = Stage<L, LR, SPLIT, E>;
+    return reinterpret_cast<const uint4 *>(img)[wave * G::kL0 * G::PC + q];
 }
-template <int L, int LR, bool SPLIT = false>
+template <int L, int LR, bool SPLIT, int E>
 __device__ __forceinline__ uint4 shared_piece(const uint32_t *img_i, const uint32_t *img_f, uint32_t q) {
-    using G = Stage<L, LR, SPLIT>;
-    const uint32_t t = q / 5, piece = q - t * 5;
+    using G = Stage<L, LR, SPLIT, E>;
+    const uint32_t t = q / G::PC, piece = q - t * G::PC;
     const uint32_t slot = t < G::kShI ? G::n - (G::n >> G::IW) + t : G::n - (G::n >> G::WB) + (t - G::kShI);
-    return reinterpret_cast<const uint4 *>(t < G::kShI ? img_i : img_f)[slot * 5u + piece];
+    return reinterpret_cast<const uint4 *>(t < G::kShI ? img_i : img_f)[slot * G::PC + piece];
 }
-// 16-byte piece q of the D tables (Stage::kD): layer b = q / 5 of image t_i ^ t_f, group 0
-template <int L, int LR, bool SPLIT = false>
+// 16-byte piece q of the D tables (Stage::kD): layer b = q / PC of image t_i ^ t_f, group 0
+template <int L, int LR, bool SPLIT, int E>
 __device__ __forceinline__ uint4 d_piece(const uint32_t *img_d, uint32_t q) {
-    using G = Stage<L, LR, SPLIT>;
-    const uint32_t b = q / 5, piece = q - b * 5;
-    return reinterpret_cast<const uint4 *>(img_d)[(G::n - (G::n >> b)) * 5u + piece];
+    using G = Stage<L, LR, SPLIT, E>;
+    const uint32_t b = q / G::PC, piece = q - b * G::PC;
+    return reinterpret_cast<const uint4 *>(img_d)[(G::n - (G::n >> b)) * G::PC + piece];
 }
 // layer of table slot t of a wave-private region (phases 1 and 3)
-template <int L, int LR, bool SPLIT = false>
+template <int L, int LR, bool SPLIT, int E>
 __device__ __forceinline__ uint32_t priv_layer(uint32_t t) {
-    using G = Stage<L, LR, SPLIT>;
+    using G = Stage<L, LR, SPLIT, E>;
     const uint32_t y = (G::W >> G::B0) - t;
     return uint32_t(G::IW - int(32 - __builtin_clz(y - 1)));
 }
@@ -1088,16 +1142,17 @@ __device__ __forceinline__ uint32_t priv_layer(uint32_t t) {
 #define RS_MONO_LDS_PF 2
 #endif
 
-template <int L, int LR, int MODE, bool STAGED, bool BATCH, bool SPLIT>
+template <int L, int LR, int MODE, bool STAGED, bool BATCH, bool SPLIT, int E>
 __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
-    using C = Col<L, LR>;
-    using G = Stage<L, LR, SPLIT>;
+    using C = Col<L, LR, E>;
+    using G = Stage<L, LR, SPLIT, E>;
     static_assert(!SPLIT || (STAGED && MODE == kMonoDecode), "split plan: staged decode only");
+    static_assert(STAGED || E == 4, "2-element packs: staged kernel only");
     constexpr int R = 1 << LR;
     constexpr uint32_t T = 1u << (L - LR);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t *plane = lds;
-    // XCD-aware: workgroup b runs on XCD b % 8, so the 8 packs of one 64-byte
+    // XCD-aware: workgroup b runs on XCD b % 8, so the packs of one 64-byte
     // block (which share cache lines) go to one XCD's L2.
 #ifdef RS_MONO_STAMPS  // entry time, before the first kernel-argument load
     if (threadIdx.x == blockDim.x - 64 && blockIdx.x < 4096) g_mono_stamps[blockIdx.x][7] = __builtin_amdgcn_s_memrealtime();
@@ -1108,7 +1163,8 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
     if (pk >= A.packs) return;
     const StripeBases sb = BATCH ? stripe_bases(A, blockIdx.y) : StripeBases{A.src[0].base, A.src[1].base,
                                                                              const_cast<uint8_t *>(A.dst.base)};
-    const PackIO io = pack_io(A.fmt, pk);  // the pack's bytes in the caller's rows (tails: shards.rs:38-74)
+    // the pack's bytes in the caller's rows (tails: shards.rs:38-74)
+    const PackIO io = E == 4 ? pack_io(A.fmt, pk) : pack_io2(A.fmt, pk);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t *img_i = A.img + uint64_t(A.ifft_img) * A.img_words;
@@ -1121,12 +1177,13 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
         constexpr bool DEC = MODE == kMonoDecode;
         uint32_t *shared = lds + G::plane_words;
         constexpr uint32_t kSh = DEC ? G::kShared : G::kShared + G::kD;  // shared tables (+ D)
-        uint32_t *priv = shared + kSh * 20 + wave * G::kPriv * 20;
+        uint32_t *priv = shared + kSh * G::TW + wave * G::kPriv * G::TW;
         uint32_t *rinfo = lds + G::words;  // decode with fused eval_poly
-        constexpr int KP1 = (5 * G::kUp + 63) / 64;
-        constexpr int KP0 = G::B0 ? (5 * G::kL0 + 63) / 64 : 1;
-        constexpr int KP3 = G::kP3 ? (5 * G::kP3 + 63) / 64 : 1;  // (guarded by q < 5 * kP3)
-        constexpr int KSH = kSh ? (5 * kSh + T - 1) / T : 1;  // (guarded by q < 5 * kSh)
+        constexpr uint32_t PC = G::PC;  // 16-byte pieces per table
+        constexpr int KP1 = (PC * G::kUp + 63) / 64;
+        constexpr int KP0 = G::B0 ? (PC * G::kL0 + 63) / 64 : 1;
+        constexpr int KP3 = G::kP3 ? (PC * G::kP3 + 63) / 64 : 1;  // (guarded by q < PC * kP3)
+        constexpr int KSH = kSh ? (PC * kSh + T - 1) / T : 1;  // (guarded by q < PC * kSh)
         RS_MSTAMP(0);
         // decode: does this wave's phase-1 row block (2^IW consecutive rows) hold a
         // received row?  If not its rows are zero through phase 1: it loads no
@@ -1163,7 +1220,7 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             lw[1] = A.lw_fold[i0 + 1];
         }
         uint32_t w[2 << LR];
-        issue_col<L, LR, SPLIT>(A, 0, io, sb, w, lane, wave, live);
+        issue_col<L, LR, SPLIT, E>(A, 0, io, sb, w, lane, wave, live);
         // phase-1 tables (a wave that skips phase 1 reads one table: no branch
         // around the loads); B0: layer 0's go into the region first, the
         // layers above when layer 0 has read them (run_seq's hook)
@@ -1172,16 +1229,16 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
         if constexpr (G::B0)
             static_for<0, KP0>([&](auto kc) {
                 const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < 5 * G::kL0) v0[kc] = l0_piece<L, LR, SPLIT>(img_i, wave, live ? q : q % 5u);
+                if (q < PC * G::kL0) v0[kc] = l0_piece<L, LR, SPLIT, E>(img_i, wave, live ? q : q % PC);
             });
         static_for<0, KP1>([&](auto kc) {
             const uint32_t q = lane + 64u * decltype(kc)::value;
-            if (q < 5 * G::kUp) v1[kc] = priv_piece<L, LR, SPLIT>(img_i, wave, live ? q : q % 5u);
+            if (q < PC * G::kUp) v1[kc] = priv_piece<L, LR, SPLIT, E>(img_i, wave, live ? q : q % PC);
         });
         static_for<0, KSH>([&](auto kc) {
             const uint32_t q = threadIdx.x + T * decltype(kc)::value;
-            if (q < 5 * G::kShared) vs[kc] = shared_piece<L, LR, SPLIT>(img_i, img_f, q);
-            else if (!DEC && q < 5 * kSh) vs[kc] = d_piece<L, LR, SPLIT>(img_d, q - 5 * G::kShared);
+            if (q < PC * G::kShared) vs[kc] = shared_piece<L, LR, SPLIT, E>(img_i, img_f, q);
+            else if (!DEC && q < PC * kSh) vs[kc] = d_piece<L, LR, SPLIT, E>(img_d, q - PC * G::kShared);
         });
 #endif
         const uint32_t *ri = A.rowinfo;
@@ -1196,13 +1253,13 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             ri = rinfo;
             RS_MSTAMP(2);
         }
-        ScaleTabs<L, LR> st;
-        if constexpr (DEC) scale_issue<L, LR, SPLIT>(A, ri, st, lane, wave);
+        ScaleTabs<L, LR, E> st;
+        if constexpr (DEC) scale_issue<L, LR, SPLIT, E>(A, ri, st, lane, wave);
         auto write1 = [&]() {
 #ifndef RS_MONO_SKIP_STAGE
             static_for<0, KP1>([&](auto kc) {
                 const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < 5 * G::kUp) reinterpret_cast<uint4 *>(priv)[q] = v1[kc];
+                if (q < PC * G::kUp) reinterpret_cast<uint4 *>(priv)[q] = v1[kc];
             });
 #endif
         };
@@ -1210,19 +1267,19 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
         if constexpr (G::B0)
             static_for<0, KP0>([&](auto kc) {
                 const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < 5 * G::kL0) reinterpret_cast<uint4 *>(priv)[q] = v0[kc];
+                if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[q] = v0[kc];
             });
         else
             write1();
         static_for<0, KSH>([&](auto kc) {
             const uint32_t q = threadIdx.x + T * decltype(kc)::value;
-            if (q < 5 * kSh) reinterpret_cast<uint4 *>(shared)[q] = vs[kc];
+            if (q < PC * kSh) reinterpret_cast<uint4 *>(shared)[q] = vs[kc];
         });
 #endif
         RS_MSTAMP(6);
         finish_col<L, LR, DEC>(w, &st, c, lane);
         RS_MSTAMP(1);
-        const LdsTabs<L, LR, SPLIT> ts{priv, shared, img_i, img_f};
+        const LdsTabs<L, LR, SPLIT, E> ts{priv, shared, img_i, img_f};
         // phase-3 tables: requested when phase 1 ends, written over this wave's
         // phase-1 tables when phase 2 ends
         uint4 v3[KP3];
@@ -1230,7 +1287,7 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             if (reuse3) return;
             static_for<0, KP3>([&](auto kc) {
                 const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < 5 * G::kP3) v3[kc] = priv_piece<L, LR, SPLIT>(img_f, wave, out_wave ? q : q % 5u);
+                if (q < PC * G::kP3) v3[kc] = priv_piece<L, LR, SPLIT, E>(img_f, wave, out_wave ? q : q % PC);
             });
         };
         auto write3 = [&]() {
@@ -1240,23 +1297,23 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
                     uint4 x[KP3];
                     static_for<0, KP3>([&](auto kc) {
                         const uint32_t q = lane + 64u * decltype(kc)::value;
-                        if (q < 5 * G::kP3) {
-                            const uint32_t t = q / 5, piece = q - t * 5;
+                        if (q < PC * G::kP3) {
+                            const uint32_t t = q / PC, piece = q - t * PC;
                             const uint4 v = reinterpret_cast<const uint4 *>(priv)[q];
-                            const uint4 d = reinterpret_cast<const uint4 *>(shared)[(G::kShared + priv_layer<L, LR, SPLIT>(t)) * 5 + piece];
+                            const uint4 d = reinterpret_cast<const uint4 *>(shared)[(G::kShared + priv_layer<L, LR, SPLIT, E>(t)) * PC + piece];
                             x[kc] = uint4{v.x ^ d.x, v.y ^ d.y, v.z ^ d.z, v.w ^ d.w};
                         }
                     });
                     static_for<0, KP3>([&](auto kc) {
                         const uint32_t q = lane + 64u * decltype(kc)::value;
-                        if (q < 5 * G::kP3) reinterpret_cast<uint4 *>(priv)[q] = x[kc];
+                        if (q < PC * G::kP3) reinterpret_cast<uint4 *>(priv)[q] = x[kc];
                     });
                 }
                 return;
             }
             static_for<0, KP3>([&](auto kc) {
                 const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < 5 * G::kP3) reinterpret_cast<uint4 *>(priv)[q] = v3[kc];
+                if (q < PC * G::kP3) reinterpret_cast<uint4 *>(priv)[q] = v3[kc];
             });
         };
         // B0: the FFT's layer-0 tables (phase 3's last layer), requested while the
@@ -1266,14 +1323,14 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             if constexpr (G::B0)
                 static_for<0, KP0>([&](auto kc) {
                     const uint32_t q = lane + 64u * decltype(kc)::value;
-                    if (q < 5 * G::kL0) v4[kc] = l0_piece<L, LR, SPLIT>(img_f, wave, need ? q : q % 5u);
+                    if (q < PC * G::kL0) v4[kc] = l0_piece<L, LR, SPLIT, E>(img_f, wave, need ? q : q % PC);
                 });
         };
         auto write4 = [&]() {
             if constexpr (G::B0)
                 static_for<0, KP0>([&](auto kc) {
                     const uint32_t q = lane + 64u * decltype(kc)::value;
-                    if (q < 5 * G::kL0) reinterpret_cast<uint4 *>(priv)[q] = v4[kc];
+                    if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[q] = v4[kc];
                 });
         };
         if constexpr (SPLIT) {
@@ -1291,7 +1348,7 @@ __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
             const bool out = out_wave;
             const bool alive = out && wave_stores<L, LR, true>(A, wave);
             constexpr uint32_t kTopI = (G::n >> G::IW) - 2, kTopF = G::kShI + (G::n >> G::WB) - 2;
-            split_top<L, LR>(c, plane, lds + G::words_dec, shared + kTopI * 20, shared + kTopF * 20, lane, wave,
+            split_top<L, LR>(c, plane, lds + G::words_dec, shared + kTopI * G::TW, shared + kTopF * G::TW, lane, wave,
                              A.out_half);
             issue4(alive);
             // FFT below the top layer: only the half that holds restored rows
@@ -1374,24 +1431,39 @@ constexpr int mono_lr(int L, bool staged) {
     return staged ? 1 : L <= 10 ? (RS_MONO_LR10 < L - 6 ? RS_MONO_LR10 : L - 6) : L - 9;
 }
 
-template <int L, int MODE, bool STAGED, bool BATCH = false, bool SPLIT = false>
+template <int L, int MODE, bool STAGED, bool BATCH = false, bool SPLIT = false, int E = 4>
 hipError_t launch_ls(const MonoArgs &A, hipStream_t s) {
     constexpr int LR = mono_lr(L, STAGED);
-    using G = Stage<L, LR, SPLIT>;
-    const size_t lds = STAGED ? size_t(SPLIT ? G::words_split : MODE == kMonoDecode ? G::words_dec : G::words_enc) * 4
-                              : size_t(8) << L;
+    using G = Stage<L, LR, SPLIT, E>;
+    size_t lds = STAGED ? size_t(SPLIT ? G::words_split : MODE == kMonoDecode ? G::words_dec : G::words_enc) * 4
+                        : size_t(8) << L;
+    // 2-element packs exist to spread a launch over more CUs: more than half the
+    // CU's LDS keeps the dispatcher from doubling workgroups up on one CU
+    if (E == 2 && lds <= 80 * 1024) lds = 84 * 1024;
     static bool attr_set = false;  // benign race: idempotent attribute call
     if (!attr_set && lds > 65536) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mono<L, LR, MODE, STAGED, BATCH, SPLIT>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mono<L, LR, MODE, STAGED, BATCH, SPLIT, E>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const uint32_t grid = 8u * A.packs_per_xcd;
-    k_mono<L, LR, MODE, STAGED, BATCH, SPLIT><<<dim3(grid, BATCH ? A.stripes : 1), 1 << (L - LR), lds, s>>>(A);
-    snprintf(launch_name_buf(), kLaunchNameBytes, "k_mono<%d, %d, %d, %s, %s, %s>", L, LR, MODE,
-             STAGED ? "true" : "false", BATCH ? "true" : "false", SPLIT ? "true" : "false");
+    k_mono<L, LR, MODE, STAGED, BATCH, SPLIT, E><<<dim3(grid, BATCH ? A.stripes : 1), 1 << (L - LR), lds, s>>>(A);
+    snprintf(launch_name_buf(), kLaunchNameBytes, "k_mono<%d, %d, %d, %s, %s, %s, %d>", L, LR, MODE,
+             STAGED ? "true" : "false", BATCH ? "true" : "false", SPLIT ? "true" : "false", E);
     return hipGetLastError();
+}
+
+template <int L, int MODE, int E>
+hipError_t launch_staged(const MonoArgs &A, hipStream_t s) {
+    if constexpr (MODE == kMonoDecode && split_l(L)) {
+        if (A.split) {
+            if (A.stripes > 1) return launch_ls<L, MODE, true, true, true, E>(A, s);
+            return launch_ls<L, MODE, true, false, true, E>(A, s);
+        }
+    }
+    if (A.stripes > 1) return launch_ls<L, MODE, true, true, false, E>(A, s);
+    return launch_ls<L, MODE, true, false, false, E>(A, s);
 }
 
 // Staged (LDS tables) variant: single-chunk transforms, 2 rows per lane.
@@ -1401,17 +1473,11 @@ hipError_t launch_l(const MonoArgs &A, hipStream_t s) {
     if constexpr (staged_l(L)) {
         if (A.chunks == 1) {  // = mono_staged()
             if (MODE == kMonoDecode && !A.fused_eval) return hipErrorInvalidValue;
-            if constexpr (MODE == kMonoDecode && split_l(L)) {
-                if (A.split) {
-                    if (A.stripes > 1) return launch_ls<L, MODE, true, true, true>(A, s);
-                    return launch_ls<L, MODE, true, false, true>(A, s);
-                }
-            }
-            if (A.stripes > 1) return launch_ls<L, MODE, true, true>(A, s);
-            return launch_ls<L, MODE, true>(A, s);
+            if (A.elems == 2) return launch_staged<L, MODE, 2>(A, s);
+            return launch_staged<L, MODE, 4>(A, s);
         }
     }
-    if (A.fused_eval || A.stripes > 1) return hipErrorInvalidValue;
+    if (A.fused_eval || A.stripes > 1 || A.elems != 4) return hipErrorInvalidValue;
     return launch_ls<L, MODE, false>(A, s);
 }
 

@@ -713,9 +713,12 @@ MONO_CASES = [
 ]
 
 
-@pytest.mark.parametrize("mono", [1, 2, 0])
+@pytest.mark.parametrize("mono", [1, 1 | 8, 1 | 16, 2, 0])
 @pytest.mark.parametrize("rate,N,M,S", MONO_CASES)
 def test_column_kernel_and_pass_paths_match_oracle(torch, rs, rate, N, M, S, mono):
+    """mono 1: default routing (2-element packs for small single-chunk launches), + 8: 4-element
+    packs only, + 16: 2-element packs for every single-chunk launch, 2: column kernel for
+    multi-chunk / 2^11-2^12 rows too, 0: pass kernels."""
     rs.mono_enable(mono)
     try:
         orig = O.generate_original(N, S, (N * 3 + M + S) & 0xFF)
@@ -915,7 +918,7 @@ def test_split_decode_matches_oracle(torch, rs, rate, N, M, S, kind):
     rp = np.zeros(M, np.uint8)
     rp[rng.choice(M, L, replace=False)] = 1
     outs = []
-    for flag in (1, 1 | 4):
+    for flag in (1, 1 | 4, 1 | 8, 1 | 4 | 8):
         rs.mono_enable(flag)
         try:
             outs.append(gpu_decode(torch, rs, rate, orig, op, rec, rp))
