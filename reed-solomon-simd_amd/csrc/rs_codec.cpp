@@ -301,11 +301,6 @@ rs::PassArgs base_args(rs_context *ctx, const Geom &g, uint32_t n) {
 // IFFT runs levels 0..m-1 ascending, the FFT m-1..0 descending; the top
 // level's IFFT + FFT are fused into one pass (DESIGN.md "Pass structure").
 constexpr uint32_t kMaxK = 8;  // pass kernels exist for K <= 8
-// Measured (profiles/r01g/sweep_k*.jsonl, profiles/r01i/, profiles/r01k/):
-// with the 512-thread wide shapes (rs_kernels.hip launch_shape), 7-bit passes
-// win for encodes (8192:8192 x 64 KiB 747 -> 857 GiB/s) and decodes (377 ->
-// 396 GiB/s); 8-bit passes only once a transform has thousands of packs
-// (32768:32768 x 64 KiB encode 820 -> 884 GiB/s; at 1 KiB shards 656 -> 505).
 constexpr uint64_t kMaxBatchStripes = 65535;  // stripes per column-kernel launch (grid.y)
 uint32_t g_max_k = 0;  // RS_MI355X_MAX_K (4..8) overrides the choice below
 // Measured with the pruned decode passes (profiles/r01p/ab_maxk_*, tools/ab_maxk.sh):

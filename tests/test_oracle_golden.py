@@ -118,3 +118,15 @@ def avx2_engine():
 def test_avx2_port_golden(case, avx2_engine):
     """The AVX2-restatement CPU baseline reproduces the reference hashes too."""
     run_case(case)
+
+
+def test_oracle_under_address_and_ub_sanitizers():
+    """oracle/Makefile `asan`: the oracle (both engines) built with -fsanitize=address,undefined
+    runs encode -> erase -> decode round trips (every rate, tail sizes, multi-chunk shapes)
+    without a sanitizer report and restores every lost shard."""
+    import subprocess
+    odir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+    subprocess.run(["make", "-s", "-C", odir, "asan"], check=True)
+    r = subprocess.run([os.path.join(odir, "_build", "asan_check")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failures" in r.stdout
