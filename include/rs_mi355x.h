@@ -88,6 +88,8 @@ typedef enum rs_rate { RS_RATE_DEFAULT = 0, RS_RATE_HIGH = 1, RS_RATE_LOW = 2 } 
 typedef struct rs_context rs_context;
 typedef struct rs_encoder rs_encoder;
 typedef struct rs_decoder rs_decoder;
+typedef struct rs_encoder_work rs_encoder_work; /* EncoderWork (src/rate/encoder_work.rs) */
+typedef struct rs_decoder_work rs_decoder_work; /* DecoderWork (src/rate/decoder_work.rs) */
 
 /* ---- context: one per device; builds and uploads the GF tables once ---- */
 rs_status rs_context_create(int device, rs_context **out);
@@ -131,6 +133,18 @@ const uint8_t *rs_encoder_recovery(rs_encoder *enc, uint64_t index);
 void rs_encoder_result_drop(rs_encoder *enc); /* EncoderResult::drop -> reset_received */
 int rs_encoder_is_high_rate(const rs_encoder *enc);
 void rs_encoder_free(rs_encoder *enc);
+/* RateEncoder::into_parts (src/rate.rs:129-131): consumes enc (freed), returns its engine
+ * (the context) and its working space (host and device buffers) for reuse by another
+ * encoder of any rate and shape.  Either out pointer may be NULL. */
+rs_status rs_encoder_into_parts(rs_encoder *enc, rs_context **ctx_out, rs_encoder_work **work_out);
+/* RateEncoder::new with `work: Option<EncoderWork>` (src/rate.rs:133-139,
+ * src/rate/rate_high.rs:93-103): like
+ * rs_encoder_new, reusing `work`'s buffers (NULL = none).  `work` is consumed in every
+ * case, also when the call fails (as when the reference's new returns Err). */
+rs_status rs_encoder_new_with_work(rs_context *ctx, rs_rate rate, uint64_t original_count,
+                                   uint64_t recovery_count, uint64_t shard_bytes, rs_encoder_work *work,
+                                   rs_encoder **out, rs_error *err);
+void rs_encoder_work_free(rs_encoder_work *work);
 
 /* ---- ReedSolomonDecoder / RateDecoder (src/reed_solomon.rs, src/rate.rs:179-250) ---- */
 rs_status rs_decoder_new(rs_context *ctx, rs_rate rate, uint64_t original_count, uint64_t recovery_count,
@@ -149,6 +163,13 @@ uint64_t rs_decoder_restored_count(const rs_decoder *dec);
 void rs_decoder_result_drop(rs_decoder *dec); /* DecoderResult::drop -> reset_received */
 int rs_decoder_is_high_rate(const rs_decoder *dec);
 void rs_decoder_free(rs_decoder *dec);
+/* RateDecoder::into_parts / new with work (src/rate.rs:206-218, src/rate/rate_high.rs:260-270):
+ * as for the encoder. */
+rs_status rs_decoder_into_parts(rs_decoder *dec, rs_context **ctx_out, rs_decoder_work **work_out);
+rs_status rs_decoder_new_with_work(rs_context *ctx, rs_rate rate, uint64_t original_count,
+                                   uint64_t recovery_count, uint64_t shard_bytes, rs_decoder_work *work,
+                                   rs_decoder **out, rs_error *err);
+void rs_decoder_work_free(rs_decoder_work *work);
 
 /* ---- device-resident batch path (HBM in, HBM out) ----
  * d_original: original_count rows, d_recovery: recovery_count rows, both

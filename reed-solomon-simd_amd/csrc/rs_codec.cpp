@@ -93,6 +93,13 @@ int resolve(rs_rate rate, uint64_t N, uint64_t M, uint64_t S, rs_error *err) {
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    void swap(DevBuf &o) {
+        std::swap(p, o.p);
+        std::swap(cap, o.cap);
+    }
     void *get(size_t bytes) {
         if (bytes > cap) {
             if (p) check(hipFree(p));
@@ -113,6 +120,14 @@ struct PinnedBuf {
     void *p = nullptr;
     size_t cap = 0;
     hipEvent_t ready = nullptr;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf &) = delete;
+    PinnedBuf &operator=(const PinnedBuf &) = delete;
+    void swap(PinnedBuf &o) {
+        std::swap(p, o.p);
+        std::swap(cap, o.cap);
+        std::swap(ready, o.ready);
+    }
     uint8_t *get(size_t bytes) {
         if (ready) check(hipEventSynchronize(ready));  // the previous copy out of it is done
         if (bytes > cap) {
@@ -140,6 +155,13 @@ struct Workspace {
     DevBuf buf[4], rowinfo, state;
     std::vector<uint8_t> h_state;
     PinnedBuf h_state_pinned;  // source of the erasure-state copy of large decodes
+    void swap(Workspace &o) {
+        for (int k = 0; k < 4; ++k) buf[k].swap(o.buf[k]);
+        rowinfo.swap(o.rowinfo);
+        state.swap(o.state);
+        h_state.swap(o.h_state);
+        h_state_pinned.swap(o.h_state_pinned);
+    }
 };
 
 // Runs the calling thread on `device` for the scope and restores the thread's
@@ -884,6 +906,37 @@ struct rs_decoder {
     Workspace ws;
 };
 
+// EncoderWork / DecoderWork (src/rate.rs:129-131, 206-208): an encoder's or
+// decoder's buffers, handed from one object to the next (any rate, any shape).
+struct rs_encoder_work {
+    std::vector<uint8_t> h_orig, h_rec;
+    DevBuf d_orig, d_rec;
+    Workspace ws;
+    void swap(rs_encoder &e) {
+        h_orig.swap(e.h_orig);
+        h_rec.swap(e.h_rec);
+        d_orig.swap(e.d_orig);
+        d_rec.swap(e.d_rec);
+        ws.swap(e.ws);
+    }
+};
+struct rs_decoder_work {
+    std::vector<uint8_t> orig_present, rec_present, h_orig, h_rec, h_out;
+    DevBuf d_orig, d_rec, d_out;
+    Workspace ws;
+    void swap(rs_decoder &d) {
+        orig_present.swap(d.orig_present);
+        rec_present.swap(d.rec_present);
+        h_orig.swap(d.h_orig);
+        h_rec.swap(d.h_rec);
+        h_out.swap(d.h_out);
+        d_orig.swap(d.d_orig);
+        d_rec.swap(d.d_rec);
+        d_out.swap(d.d_out);
+        ws.swap(d.ws);
+    }
+};
+
 namespace {
 
 // tail re-pack of a shard into padded 64-byte blocks (shards.rs:38-59)
@@ -1341,11 +1394,18 @@ rs_status rs_decode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint
 
 rs_status rs_encoder_new(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, rs_encoder **out,
                          rs_error *err) {
+    return rs_encoder_new_with_work(ctx, rate, N, M, S, nullptr, out, err);
+}
+
+rs_status rs_encoder_new_with_work(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S,
+                                   rs_encoder_work *work, rs_encoder **out, rs_error *err) {
+    std::unique_ptr<rs_encoder_work> w(work);  // consumed in every case (moved into `new`, rate.rs:133-139)
     if (!ctx || !out) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     *out = nullptr;
     auto *e = new rs_encoder;
     e->ctx = ctx;
     e->rate = rate;
+    if (w) w->swap(*e);
     const rs_status st = encoder_configure(e, N, M, S, err);
     if (st != RS_OK) {
         delete e;
@@ -1415,15 +1475,35 @@ void rs_encoder_result_drop(rs_encoder *e) {
 int rs_encoder_is_high_rate(const rs_encoder *e) { return e ? e->high : -1; }
 void rs_encoder_free(rs_encoder *e) { delete e; }
 
+rs_status rs_encoder_into_parts(rs_encoder *e, rs_context **ctx_out, rs_encoder_work **work_out) {
+    if (!e) return RS_ERR_INVALID_ARGUMENT;
+    auto *w = new rs_encoder_work;
+    w->swap(*e);
+    if (ctx_out) *ctx_out = e->ctx;
+    if (work_out) *work_out = w;
+    else delete w;
+    delete e;
+    return RS_OK;
+}
+
+void rs_encoder_work_free(rs_encoder_work *w) { delete w; }
+
 // ---- decoder ----------------------------------------------------------------
 
 rs_status rs_decoder_new(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S, rs_decoder **out,
                          rs_error *err) {
+    return rs_decoder_new_with_work(ctx, rate, N, M, S, nullptr, out, err);
+}
+
+rs_status rs_decoder_new_with_work(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, uint64_t S,
+                                   rs_decoder_work *work, rs_decoder **out, rs_error *err) {
+    std::unique_ptr<rs_decoder_work> w(work);  // consumed in every case
     if (!ctx || !out) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     *out = nullptr;
     auto *d = new rs_decoder;
     d->ctx = ctx;
     d->rate = rate;
+    if (w) w->swap(*d);
     const rs_status st = decoder_configure(d, N, M, S, err);
     if (st != RS_OK) {
         delete d;
@@ -1527,6 +1607,19 @@ void rs_decoder_result_drop(rs_decoder *d) {
 }
 int rs_decoder_is_high_rate(const rs_decoder *d) { return d ? d->high : -1; }
 void rs_decoder_free(rs_decoder *d) { delete d; }
+
+rs_status rs_decoder_into_parts(rs_decoder *d, rs_context **ctx_out, rs_decoder_work **work_out) {
+    if (!d) return RS_ERR_INVALID_ARGUMENT;
+    auto *w = new rs_decoder_work;
+    w->swap(*d);
+    if (ctx_out) *ctx_out = d->ctx;
+    if (work_out) *work_out = w;
+    else delete w;
+    delete d;
+    return RS_OK;
+}
+
+void rs_decoder_work_free(rs_decoder_work *w) { delete w; }
 
 // ---- one-shot (lib.rs:251-353) -------------------------------------------------
 

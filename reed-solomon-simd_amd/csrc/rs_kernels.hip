@@ -721,7 +721,7 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
 // SIMD (<= 80 VGPRs) so that three of its workgroups share a CU: one's row
 // loads and stores overlap the others' layers.
 template <int LR, int FLAGS>
-constexpr int pass_waves_per_eu() { return FLAGS == (kIfft | kFft) && LR >= 3 ? 6 : 2; }
+constexpr int pass_waves_per_eu() { return FLAGS == (kIfft | kFft) && LR == 3 ? 6 : 2; }
 
 template <int K, int LR, int SPL, int FLAGS>
 __global__ void __launch_bounds__(1 << (K - LR + SPL), (pass_waves_per_eu<LR, FLAGS>())) k_pass(const PassArgs A) {
@@ -786,6 +786,8 @@ hipError_t launch_k(int flags, const PassArgs &A, hipStream_t s) {
 // over more workgroups and waves.
 template <int K>
 hipError_t launch_shape(bool narrow, int flags, const PassArgs &A, hipStream_t s) {
+    // (16 rows per lane at K = 7, 8 -- two phases, one exchange -- measured slower at
+    // configs 3 and 5: 1 workgroup per CU; tools/ab_variant.sh)
     constexpr int LRW = K < 3 ? K : 3;
     constexpr int SPLW = K >= 8 ? 4 : K == 7 ? 5 : 6;
     if constexpr (K >= 2) {

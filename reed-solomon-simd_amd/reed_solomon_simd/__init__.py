@@ -23,7 +23,8 @@ import os
 from typing import Dict, Iterable, List, Optional, Tuple
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librs_mi355x.so")
+# RS_MI355X_LIB: an alternative build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("RS_MI355X_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "librs_mi355x.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -78,6 +79,12 @@ _sig("rs_encoder_result_drop", None, _vp)
 _sig("rs_encoder_is_high_rate", _int, _vp)
 _sig("rs_encoder_free", None, _vp)
 _sig("rs_decoder_new", _int, _vp, _int, _u64, _u64, _u64, ctypes.POINTER(_vp), _E)
+_sig("rs_encoder_new_with_work", _int, _vp, _int, _u64, _u64, _u64, _vp, ctypes.POINTER(_vp), _E)
+_sig("rs_decoder_new_with_work", _int, _vp, _int, _u64, _u64, _u64, _vp, ctypes.POINTER(_vp), _E)
+_sig("rs_encoder_into_parts", _int, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp))
+_sig("rs_decoder_into_parts", _int, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp))
+_sig("rs_encoder_work_free", None, _vp)
+_sig("rs_decoder_work_free", None, _vp)
 _sig("rs_decoder_reset", _int, _vp, _u64, _u64, _u64, _E)
 _sig("rs_decoder_add_original_shard", _int, _vp, _u64, ctypes.c_char_p, _u64, _E)
 _sig("rs_decoder_add_recovery_shard", _int, _vp, _u64, ctypes.c_char_p, _u64, _E)
@@ -403,15 +410,48 @@ class DecoderResult:
             pass
 
 
+class _Work:
+    """EncoderWork / DecoderWork (src/rate.rs:129-131, 206-208): the buffers of a consumed
+    encoder / decoder (into_parts), reusable by a new one of any rate and shape (work=...)."""
+    _FREE = None
+
+    def __init__(self, handle):
+        self._h = handle
+
+    def _take(self):
+        h, self._h = self._h, None
+        if h is None:
+            raise ValueError("this work object was already handed to an encoder / decoder")
+        return h
+
+    def __del__(self):
+        try:
+            if self._h:
+                getattr(_lib, self._FREE)(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+class EncoderWork(_Work):
+    _FREE = "rs_encoder_work_free"
+
+
+class DecoderWork(_Work):
+    _FREE = "rs_decoder_work_free"
+
+
 class _EncoderBase:
     RATE = RATE_DEFAULT
 
-    def __init__(self, original_count: int, recovery_count: int, shard_bytes: int, ctx: Optional[Context] = None):
+    def __init__(self, original_count: int, recovery_count: int, shard_bytes: int, ctx: Optional[Context] = None,
+                 work: Optional[EncoderWork] = None):
         self._ctx = ctx or default_context()
         h = _vp()
         err = _RsError()
-        code = _lib.rs_encoder_new(self._ctx.handle, self.RATE, original_count, recovery_count, shard_bytes,
-                                   ctypes.byref(h), ctypes.byref(err))
+        w = work._take() if work is not None else None  # consumed in every case (rate_high.rs:93-103)
+        code = _lib.rs_encoder_new_with_work(self._ctx.handle, self.RATE, original_count, recovery_count,
+                                             shard_bytes, w, ctypes.byref(h), ctypes.byref(err))
         _raise(code, err)
         self._h = h
         self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
@@ -457,6 +497,15 @@ class _EncoderBase:
     def is_high_rate(self) -> bool:
         return bool(_lib.rs_encoder_is_high_rate(self._h))
 
+    def into_parts(self):
+        """RateEncoder::into_parts (src/rate.rs:129-131): consumes this encoder, returns
+        (engine context, EncoderWork)."""
+        self._drop_result()
+        w = _vp()
+        _lib.rs_encoder_into_parts(self._h, None, ctypes.byref(w))
+        self._h = None
+        return self._ctx, EncoderWork(w)
+
     def __del__(self):
         try:
             if self._h:
@@ -469,12 +518,14 @@ class _EncoderBase:
 class _DecoderBase:
     RATE = RATE_DEFAULT
 
-    def __init__(self, original_count: int, recovery_count: int, shard_bytes: int, ctx: Optional[Context] = None):
+    def __init__(self, original_count: int, recovery_count: int, shard_bytes: int, ctx: Optional[Context] = None,
+                 work: Optional[DecoderWork] = None):
         self._ctx = ctx or default_context()
         h = _vp()
         err = _RsError()
-        code = _lib.rs_decoder_new(self._ctx.handle, self.RATE, original_count, recovery_count, shard_bytes,
-                                   ctypes.byref(h), ctypes.byref(err))
+        w = work._take() if work is not None else None
+        code = _lib.rs_decoder_new_with_work(self._ctx.handle, self.RATE, original_count, recovery_count,
+                                             shard_bytes, w, ctypes.byref(h), ctypes.byref(err))
         _raise(code, err)
         self._h = h
         self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
@@ -523,6 +574,15 @@ class _DecoderBase:
     @property
     def is_high_rate(self) -> bool:
         return bool(_lib.rs_decoder_is_high_rate(self._h))
+
+    def into_parts(self):
+        """RateDecoder::into_parts (src/rate.rs:206-208): consumes this decoder, returns
+        (engine context, DecoderWork)."""
+        self._drop_result()
+        w = _vp()
+        _lib.rs_decoder_into_parts(self._h, None, ctypes.byref(w))
+        self._h = None
+        return self._ctx, DecoderWork(w)
 
     def __del__(self):
         try:

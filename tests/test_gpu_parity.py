@@ -1066,3 +1066,46 @@ def test_batch_with_tail_shards(torch, rs, rate, N, M, S, B):
     got = d_r.cpu().numpy()
     for b in range(B):
         assert np.array_equal(got[b], O.encode(rate, origs[b], M)), f"stripe {b}"
+
+
+def test_work_handoff_between_encoders_and_decoders(rs):
+    """RateEncoder/RateDecoder::into_parts -> new(.., Some(work)) (src/rate.rs:129-139, 206-218; the
+    DefaultRate reset path, rate_default.rs:170-195): a consumed encoder's buffers serve a new
+    encoder of another rate and shape, the same for decoders; a failing `new` consumes the work."""
+    def encode_with(cls, n, m, s, seed, work=None):
+        orig = O.generate_original(n, s, seed)
+        enc = cls(n, m, s, work=work)
+        for row in orig:
+            enc.add_original_shard(row.tobytes())
+        rec = b"".join(enc.encode().recovery_iter())
+        assert rec == O.encode({rs.rate.HighRateEncoder: "high", rs.rate.LowRateEncoder: "low",
+                                rs.ReedSolomonEncoder: "default"}[cls], orig, m).tobytes()
+        return enc, orig, rec
+
+    enc, _, _ = encode_with(rs.rate.HighRateEncoder, 100, 37, 128, 1)
+    ctx, work = enc.into_parts()
+    assert ctx is not None
+    enc2, _, _ = encode_with(rs.rate.LowRateEncoder, 37, 100, 64, 2, work=work)
+    _, work2 = enc2.into_parts()
+    with pytest.raises(rs.InvalidShardSize):
+        rs.ReedSolomonEncoder(3, 2, 7, work=work2)  # consumed although new fails
+    with pytest.raises(ValueError):
+        rs.ReedSolomonEncoder(3, 2, 64, work=work2)
+    enc3, orig3, rec3 = encode_with(rs.ReedSolomonEncoder, 3, 5, 130, 3)
+
+    dec = rs.rate.LowRateDecoder(3, 5, 130)
+    dec.add_original_shard(1, orig3[1].tobytes())
+    for i in range(2):
+        dec.add_recovery_shard(i, rec3[130 * i:130 * (i + 1)])
+    out = dec.decode()
+    assert out.restored_original(0) == orig3[0].tobytes() and out.restored_original(2) == orig3[2].tobytes()
+    _, dwork = dec.into_parts()
+    orig = O.generate_original(1000, 256, 9)
+    rec = O.encode("high", orig, 100)
+    dec2 = rs.rate.HighRateDecoder(1000, 100, 256, work=dwork)
+    for i in range(100, 1000):
+        dec2.add_original_shard(i, orig[i].tobytes())
+    for i in range(100):
+        dec2.add_recovery_shard(i, rec[i].tobytes())
+    restored = dict(dec2.decode().restored_original_iter())
+    assert all(restored[i] == orig[i].tobytes() for i in range(100))

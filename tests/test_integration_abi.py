@@ -23,6 +23,11 @@ TYPES = {
     "*mut u16": "uint16_t *", "*const c_char": "const char *", "*mut RsError": "rs_error *",
     "u64": "uint64_t", "u32": "uint32_t", "u16": "uint16_t", "u8": "uint8_t", "i32": "int32_t",
     "c_int": "int", "RsStatus": "rs_status", "RsRate": "rs_rate",
+    "*mut RsEncoder": "rs_encoder *", "*mut *mut RsEncoder": "rs_encoder **",
+    "*mut RsDecoder": "rs_decoder *", "*mut *mut RsDecoder": "rs_decoder **",
+    "*mut RsEncoderWork": "rs_encoder_work *", "*mut *mut RsEncoderWork": "rs_encoder_work **",
+    "*mut RsDecoderWork": "rs_decoder_work *", "*mut *mut RsDecoderWork": "rs_decoder_work **",
+    "*mut *mut RsContext": "rs_context **",
 }
 
 

@@ -3,7 +3,7 @@ import glob
 import json
 import sys
 
-for f in sorted(glob.glob(f"gpurun_out/{sys.argv[1]}/c*.json")):
+for f in sorted(glob.glob(f"gpurun_out/{sys.argv[1]}/c*.json") + glob.glob(f"gpurun_out/{sys.argv[1]}/*/c*.json")):
     d = json.loads(open(f).read().strip().splitlines()[-1])
     r = d["roofline"]
     dec = {k: v for k, v in d.get("decode_GiBps", {}).items() if k in ("1pct", "100pct")}
