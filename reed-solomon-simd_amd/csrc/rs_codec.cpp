@@ -155,12 +155,19 @@ struct Workspace {
     DevBuf buf[4], rowinfo, state;
     std::vector<uint8_t> h_state;
     PinnedBuf h_state_pinned;  // source of the erasure-state copy of large decodes
+    // pair encode hand-off granules (rs_mono.hip pair_top): zeroed once when
+    // allocated; every pair launch on this stream tags its granules with the
+    // next epoch, so granules of earlier launches never match
+    DevBuf xchg;
+    uint32_t pair_epoch = 0;
     void swap(Workspace &o) {
         for (int k = 0; k < 4; ++k) buf[k].swap(o.buf[k]);
         rowinfo.swap(o.rowinfo);
         state.swap(o.state);
         h_state.swap(o.h_state);
         h_state_pinned.swap(o.h_state_pinned);
+        xchg.swap(o.xchg);
+        std::swap(pair_epoch, o.pair_epoch);
     }
 };
 
@@ -200,6 +207,14 @@ struct rs_context {
     uint32_t e2_max_packs = 192;
     bool e2_encode = false;
     uint32_t *d_lut2 = nullptr;   // perm2_by_log: the 2-element form of d_lut
+    // pair encode (rs_mono.hip pair_top): one-chunk encodes of 2^9 .. 2^11 rows over
+    // at most pair_max_packs packs as two workgroups per pack.  Off by default:
+    // measured no faster at the headline (k_mono_pair<9> 8.71 us vs k_mono<10>
+    // 8.68 us per launch, profiles/r02g/ab_pair: the in-launch hand-off costs what
+    // the halved workgroups save).  RS_MI355X_PAIR=1 / rs_mono_enable + 32 turn it on.
+    bool pair = false;
+    uint32_t pair_max_packs = 128;
+    uint32_t *d_pair_timeouts = nullptr;  // bounded-spin give-ups of the pair kernel (must stay 0)
     std::mutex img_mu;            // guards d_img, d_img2
     uint32_t *d_img[13] = {};     // column-kernel twiddle images per L (built at context creation)
     uint32_t *d_img2[13] = {};    // the same in the 2-element table format
@@ -447,6 +462,51 @@ void launch_mono(int mode, uint32_t L, const rs::MonoArgs &M, hipStream_t s, uin
     if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), bytes);
 }
 
+// Pair encode (rs_mono.hip pair_top, MonoArgs "Pair encode"): a one-chunk,
+// one-stripe encode of 2^L rows over few packs -- whose one workgroup per pack
+// would leave CUs idle -- runs as two workgroups per pack, one per half of
+// the rows.  Not inside a stream capture: a replayed graph would reuse the
+// launch's hand-off epoch.
+bool use_pair(rs_context *ctx, uint32_t L, const Geom &g, uint32_t chunks, hipStream_t s) {
+    if (!ctx->pair || !ctx->mono || ctx->e2_encode || chunks != 1 || g.stripes != 1) return false;
+    if (g.packs > ctx->pair_max_packs || int(L) - 1 < rs::kMonoPairMinL || int(L) - 1 > rs::kMonoPairMaxL) return false;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    check(hipStreamIsCapturing(s, &cs));
+    return cs == hipStreamCaptureStatusNone;
+}
+
+// ti / tf: skew offsets of the IFFT / FFT in units of n = 2^L.
+void launch_pair(rs_context *ctx, Workspace &ws, int mode, uint32_t L, const Geom &g, rs::MonoArgs Mo, uint32_t ti,
+                 uint32_t tf, hipStream_t s, uint64_t bytes) {
+    const uint32_t Lh = L - 1;  // rows per workgroup: 2^Lh
+    const rs::MonoArgs base = mono_args(ctx, Lh, g, true);
+    Mo.img = base.img;
+    Mo.img_words = base.img_words;
+    Mo.ifft_img = 2 * ti;
+    Mo.fft_img = 2 * tf;
+    // table of mI + mF, the two top-layer twiddles (layer L-1, group 0: skew index
+    // 2^(L-1) + t * 2^L - 1)
+    const rs::GfTables &T = rs::tables();
+    const size_t ii = (size_t(1) << (L - 1)) + size_t(ti) * (size_t(1) << L) - 1;
+    const size_t fi = (size_t(1) << (L - 1)) + size_t(tf) * (size_t(1) << L) - 1;
+    for (int q = 0; q < int(rs::kPermWords); ++q)
+        Mo.top[q] = T.perm_by_skew[ii * rs::kPermWords + q] ^ T.perm_by_skew[fi * rs::kPermWords + q];
+    // granules: 2 halves x 8 x packs_per_xcd pairs x threads x 4 (2 rows x 2 words)
+    const size_t need = size_t(16) * Mo.packs_per_xcd * (size_t(1) << (Lh - 1)) * 4 * 8;
+    if (ws.xchg.cap < need) {
+        ws.xchg.get(need);
+        check(hipMemsetAsync(ws.xchg.p, 0, need, s));
+    }
+    Mo.xchg = static_cast<uint64_t *>(ws.xchg.p);
+    if (++ws.pair_epoch == 0) ws.pair_epoch = 1;  // (2^32 launches later) never 0
+    Mo.epoch = ws.pair_epoch;
+    Mo.pair_timeouts = ctx->d_pair_timeouts;
+    hipEvent_t ev = nullptr;
+    if (t_prof_ctx) prof_begin(s, &ev);
+    check(rs::launch_mono_pair(mode, int(Lh), Mo, s));
+    if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), bytes);
+}
+
 // HighRate encode (rate_high.rs:44-87) from device rows to device rows:
 // chunk c's IFFT uses skew_delta c*n + n, the chunks are XOR-folded, one FFT
 // with skew_delta 0 produces the recovery rows.
@@ -477,6 +537,10 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
         Mo.ifft_img = 1;  // chunk c: skew offset c * n + n
         Mo.ifft_img_step = 1;
         Mo.fft_img = 0;
+        if (use_pair(ctx, L, g, C, s)) {
+            launch_pair(ctx, ws, rs::kMonoEncodeHigh, L, g, Mo, 1, 0, s, (N + M) * uint64_t(g.packs) * 8);
+            return;
+        }
         launch_mono(rs::kMonoEncodeHigh, L, Mo, s, (N + M) * uint64_t(g.packs) * 8 * g.stripes);
         return;
     }
@@ -541,6 +605,10 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
         Mo.ifft_img = 0;
         Mo.fft_img = 1;  // output chunk c: skew offset c * n + n
         Mo.fft_img_step = 1;
+        if (use_pair(ctx, L, g, C, s)) {
+            launch_pair(ctx, ws, rs::kMonoEncodeLow, L, g, Mo, 0, 1, s, (N + M) * uint64_t(g.packs) * 8);
+            return;
+        }
         launch_mono(rs::kMonoEncodeLow, L, Mo, s, (N + M) * uint64_t(g.packs) * 8 * g.stripes);
         return;
     }
@@ -1038,6 +1106,10 @@ rs_status rs_context_create(int device, rs_context **out) {
         check(hipMemcpy(ctx->d_lwfold, T.lw_fold.data(), T.lw_fold.size() * 2, hipMemcpyHostToDevice));
         check(hipMalloc(&ctx->d_lut2, T.perm2_by_log.size() * 4));
         check(hipMemcpy(ctx->d_lut2, T.perm2_by_log.data(), T.perm2_by_log.size() * 4, hipMemcpyHostToDevice));
+        check(hipMalloc(&ctx->d_pair_timeouts, 4));
+        check(hipMemset(ctx->d_pair_timeouts, 0, 4));
+        const char *np = getenv("RS_MI355X_PAIR");
+        ctx->pair = np && np[0] == '1';
         ctx->lw0 = T.log_walsh[0];
         const char *nm = getenv("RS_MI355X_NO_MONO");
         ctx->mono = !(nm && nm[0] == '1');
@@ -1072,6 +1144,7 @@ void rs_context_destroy(rs_context *ctx) {
     if (ctx->d_tw) (void)hipFree(ctx->d_tw);
     if (ctx->d_lut) (void)hipFree(ctx->d_lut);
     if (ctx->d_lut2) (void)hipFree(ctx->d_lut2);
+    if (ctx->d_pair_timeouts) (void)hipFree(ctx->d_pair_timeouts);
     for (uint32_t *p : ctx->d_img2)
         if (p) (void)hipFree(p);
     if (ctx->d_lwfold) (void)hipFree(ctx->d_lwfold);
@@ -1827,6 +1900,7 @@ rs_status rs_mono_enable(rs_context *ctx, int enable) {
     // + 8: 4-element packs only; + 16: 2-element packs wherever the staged kernel runs
     ctx->e2_max_packs = (enable & 8) ? 0u : (enable & 16) ? 0xFFFFFFFFu : 192u;
     ctx->e2_encode = (enable & 16) != 0;
+    ctx->pair = (enable & 32) != 0;  // + 32: pair encode
     return RS_OK;
 }
 
@@ -1836,6 +1910,13 @@ rs_status rs_check_device(rs_context *ctx) {
         DeviceGuard dg(ctx->device);
         check(hipDeviceSynchronize());
         check(hipGetLastError());
+        uint32_t give_ups = 0;
+        check(hipMemcpy(&give_ups, ctx->d_pair_timeouts, 4, hipMemcpyDeviceToHost));
+        if (give_ups) {
+            g_last_error = "pair encode: " + std::to_string(give_ups) +
+                           " waves gave up waiting for their partner workgroup's half (results invalid)";
+            return RS_ERR_DEVICE;
+        }
         return RS_OK;
     });
 }

@@ -419,6 +419,65 @@ def test_engine_host_slices_match_oracle(torch, rs, which):
         assert np.array_equal(got, want)
 
 
+# ---------------------------------------------------------------------------
+# pair encode (rs_mono.hip pair_top): one-chunk encodes of 2^9 .. 2^11 rows over
+# at most 128 packs run as two workgroups per pack with an in-launch hand-off
+
+PAIR_CASES = [
+    # (rate, N, M, S): 2^9, 2^10, 2^11 transform rows; tails; 1 .. 128 packs
+    ("high", 300, 300, 64), ("high", 512, 512, 1024), ("default", 1024, 1024, 1024),
+    ("high", 700, 1000, 256), ("high", 1000, 1000, 8), ("high", 2048, 2048, 64),
+    ("high", 1500, 2000, 1000), ("low", 1000, 1000, 512), ("low", 400, 300, 136),
+    ("low", 2000, 1200, 64), ("high", 1024, 1024, 2),
+]
+
+
+@pytest.mark.parametrize("rate,N,M,S", PAIR_CASES)
+def test_pair_encode_matches_oracle(torch, rs, rate, N, M, S):
+    """The pair kernel (rs_mono_enable + 32) bit-exact against the oracle, and the default
+    (one workgroup per pack) likewise."""
+    orig = O.generate_original(N, S, (N + 7 * M + S) & 0xFF)
+    want = O.encode(rate, orig, M)
+    rs.mono_enable(1 | 32)
+    try:
+        got = gpu_encode(torch, rs, rate, orig, M)
+        rs.check_device()  # also fails if a pair workgroup gave up waiting for its partner
+    finally:
+        rs.mono_enable(1)
+    assert np.array_equal(got, want)
+    assert np.array_equal(gpu_encode(torch, rs, rate, orig, M), want)
+
+
+def test_pair_encode_under_uneven_load(torch, rs):
+    """Pair hand-offs while another stream keeps the CUs busy with a large multi-pass
+    encode (partners dispatched at different times, consumers L1-warm from the previous
+    round's reads of the same granule lines): 60 back-to-back pair encodes of
+    alternating inputs on one stream, every result checked."""
+    N, M, S = 1024, 1024, 1024
+    origs = [O.generate_original(N, S, k) for k in (11, 12)]
+    wants = [O.encode("high", o, M) for o in origs]
+    d_o = [_dev(torch, o) for o in origs]
+    outs = [torch.empty((M, S), dtype=torch.uint8, device="cuda") for _ in range(60)]
+    big_n, big_s = 16384, 4096
+    b_o = torch.randint(0, 256, (big_n, big_s), dtype=torch.uint8, device="cuda")
+    b_r = torch.empty((big_n, big_s), dtype=torch.uint8, device="cuda")
+    s_big, s_pair = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    rs.mono_enable(1 | 32)
+    try:
+        for rep in range(3):
+            rs.encode_device(big_n, big_n, big_s, b_o, b_r, stream=s_big)
+            for k in range(20):
+                j = rep * 20 + k
+                rs.encode_device(N, M, S, d_o[j & 1], outs[j], stream=s_pair)
+        torch.cuda.synchronize()
+        rs.check_device()
+    finally:
+        rs.mono_enable(1)
+    for j, o in enumerate(outs):
+        assert np.array_equal(o.cpu().numpy(), wants[j & 1]), f"encode {j}"
+
+
 def test_two_streams_share_one_context(torch, rs):
     """Device scratch is per (context, stream): encodes and decodes that need scratch (pass
     kernels, 4096-row transforms) alternate between two streams of one context without a
