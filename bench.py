@@ -429,7 +429,8 @@ def sharded_bench(args, rs, ctx, world, rank, dev):
     """SURVEY.md 8(e), DESIGN.md "Multi-GPU": rank r encodes byte columns [r*w, (r+1)*w),
     w = 64 KiB / world, of its resident column slice of the originals, and an all-gather (RCCL
     over xGMI) assembles the whole [M x S] recovery matrix on every rank
-    (reed_solomon_simd.ShardedEncoder).  Total work is fixed: strong scaling.  Reported: the
+    (reed_solomon_simd.ShardedEncoder; at N > 1 in pieces whose all-gathers overlap the next
+    piece's encode and the previous one's interleave).  Total work is fixed: strong scaling.  Reported: the
     whole step (encode + all-gather + re-interleave) and encode alone."""
     import torch
 
@@ -447,9 +448,10 @@ def sharded_bench(args, rs, ctx, world, rank, dev):
     compute = rs.encode_device_call(N, M, w, d_orig, part, stream=stream, ctx=ctx)
 
     def step():
-        compute()
         if world > 1:
-            shard.gather(d_rec)
+            shard(d_orig, d_rec)  # pieces of the slice: encode, all-gather and interleave pipelined
+        else:
+            compute()
 
     t_step = timed(step, args.steps, args.warmup) / args.steps
     t_comp = timed(compute, args.steps, args.warmup) / args.steps
@@ -471,6 +473,7 @@ def sharded_bench(args, rs, ctx, world, rank, dev):
                        "parallelism": f"column partition x{world} + all_gather_into_tensor (RCCL)"},
             "encode_only": {"ms_per_step": round(t_comp * 1e3, 4), "GiBps": round(total / t_comp / 2**30, 3)},
             "allgather_and_interleave_ms": round((t_step - t_comp) * 1e3, 4),
+            "pipeline_pieces": shard.chunks if world > 1 else 1,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }))

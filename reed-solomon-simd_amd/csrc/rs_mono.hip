@@ -772,6 +772,9 @@ __device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *row
             if (keep) {
                 uint8_t *p = sb.dst + uint64_t(r - A.dst.row_begin) * A.dst.stride;
                 if constexpr (E == 2) st_half(p + off, w[j], io);
+#ifndef RS_MONO_NO_NT_STORE  // streaming (non-temporal) row stores: profiles/r02g/ab_nt
+                else if (!io.bytes) __builtin_nontemporal_store(w[j], reinterpret_cast<uint32_t *>(p + off));
+#endif
                 else st_word(p + off, w[j], io);
             }
         }

@@ -911,12 +911,18 @@ class ShardedEncoder:
     (rs_encode_device_strided) into a [recovery_count x w] slice, and an all-gather (RCCL over
     xGMI for the "nccl" backend) plus a re-interleave assembles the whole [recovery_count x
     shard_bytes] recovery matrix on every rank.  Every engine op is column-wise, so the result
-    equals a single-device encode.  The slice and gather buffers are allocated once per
-    encoder.  `encode_slice(orig_cols, rec_slice)` replaces the per-slice device encode (tests
-    drive this plumbing on CPU with a stand-in)."""
+    equals a single-device encode.
+
+    Pipelined (`chunks` > 1): the slice is encoded in `chunks` column pieces; piece c's
+    all-gather (asynchronous, on the collective's own stream) runs while piece c+1 is encoded
+    and piece c-1 is re-interleaved, so the link-bound all-gather hides the encode and the
+    interleave copies.  Buffers are allocated once per encoder.  `encode_slice(orig_cols,
+    rec_slice)` replaces the per-piece device encode (tests drive this plumbing on CPU with a
+    stand-in)."""
 
     def __init__(self, original_count: int, recovery_count: int, shard_bytes: int, device=None, group=None,
-                 stream=None, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None, encode_slice=None):
+                 stream=None, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None, encode_slice=None,
+                 chunks: Optional[int] = None):
         import torch
         import torch.distributed as dist
 
@@ -927,46 +933,78 @@ class ShardedEncoder:
                              f"{self.world} ranks")
         self.N, self.M, self.S = original_count, recovery_count, shard_bytes
         self.w = shard_bytes // self.world
+        if chunks is None:  # pieces of at least 2 KiB of columns, at most 4
+            chunks = max(c for c in (1, 2, 4) if self.w % (64 * c) == 0 and (c == 1 or self.w // c >= 2048))
+        if chunks < 1 or self.w % (64 * chunks):
+            raise ValueError(f"{chunks} pieces do not split a {self.w}-byte column slice into whole 64-byte blocks")
+        self.chunks, self.cw = chunks, self.w // chunks
         self.stream, self.rate, self.ctx = stream, rate_, ctx
         self._encode_slice = encode_slice
         self.nccl = dist.get_backend(group) == "nccl"
         dev = torch.device(device) if device is not None else (
             torch.device("cuda", torch.cuda.current_device()) if self.nccl else torch.device("cpu"))
         self.part = torch.empty((recovery_count, self.w), dtype=torch.uint8, device=dev)
-        self.gathered = (torch.empty((self.world, recovery_count, self.w), dtype=torch.uint8, device=dev)
-                         if self.world > 1 else None)
+        self.pieces = ([torch.empty((recovery_count, self.cw), dtype=torch.uint8, device=dev)
+                        for _ in range(chunks)] if self.world > 1 else [])
+        self.gathered = ([torch.empty((self.world, recovery_count, self.cw), dtype=torch.uint8, device=dev)
+                          for _ in range(chunks)] if self.world > 1 else [])
 
     def columns(self, d_original):
         """This rank's column slice of a full [N x S] original matrix (a strided view)."""
         return d_original[:, self.rank * self.w:(self.rank + 1) * self.w]
 
-    def encode_local(self, orig_cols) -> None:
-        """Encode this rank's [N x w] columns into self.part."""
+    def _encode(self, cols, out) -> None:
         if self._encode_slice is not None:
-            self._encode_slice(orig_cols, self.part)
+            self._encode_slice(cols, out)
             return
-        encode_device(self.N, self.M, self.w, orig_cols, self.part, stream=self.stream, rate_=self.rate,
-                      ctx=self.ctx)
+        encode_device(self.N, self.M, cols.shape[1], cols, out, stream=self.stream, rate_=self.rate, ctx=self.ctx)
         if self.stream is not None:
             import torch
-            torch.cuda.current_stream().wait_stream(self.stream)  # collectives run on the current stream
+            torch.cuda.current_stream().wait_stream(self.stream)  # collectives follow the current stream
+
+    def encode_local(self, orig_cols) -> None:
+        """Encode this rank's [N x w] columns into self.part (one device call)."""
+        self._encode(orig_cols, self.part)
 
     def gather(self, d_recovery) -> None:
-        """All-gather every rank's slice and re-interleave into d_recovery [M x S]."""
-        import torch.distributed as dist
-
+        """All-gather every rank's self.part and re-interleave into d_recovery [M x S]."""
         if self.world == 1:
             d_recovery.copy_(self.part)
             return
+        for c in range(self.chunks):
+            self.pieces[c].copy_(self.part[:, c * self.cw:(c + 1) * self.cw])
+        self._gather_pieces(d_recovery, range(self.chunks))
+
+    def _start_gather(self, c):
+        import torch.distributed as dist
+
         if self.nccl:
-            dist.all_gather_into_tensor(self.gathered, self.part, group=self.group)
-        else:
-            dist.all_gather(list(self.gathered.unbind(0)), self.part, group=self.group)
-        d_recovery.view(self.M, self.world, self.w).copy_(self.gathered.permute(1, 0, 2))
+            return dist.all_gather_into_tensor(self.gathered[c], self.pieces[c], group=self.group, async_op=True)
+        return dist.all_gather(list(self.gathered[c].unbind(0)), self.pieces[c], group=self.group, async_op=True)
+
+    def _finish_gather(self, work, c, d_recovery) -> None:
+        work.wait()  # (nccl: the current stream waits for the collective's stream)
+        out = d_recovery.view(self.M, self.world, self.w)[:, :, c * self.cw:(c + 1) * self.cw]
+        out.copy_(self.gathered[c].permute(1, 0, 2))
+
+    def _gather_pieces(self, d_recovery, pieces) -> None:
+        works = [(c, self._start_gather(c)) for c in pieces]
+        for c, work in works:
+            self._finish_gather(work, c, d_recovery)
 
     def __call__(self, orig_cols, d_recovery) -> None:
-        self.encode_local(orig_cols)
-        self.gather(d_recovery)
+        """Encode this rank's [N x w] columns and assemble d_recovery [M x S] on every rank."""
+        if self.world == 1:
+            self._encode(orig_cols, d_recovery)
+            return
+        pending = None
+        for c in range(self.chunks):
+            self._encode(orig_cols[:, c * self.cw:(c + 1) * self.cw], self.pieces[c])
+            work = self._start_gather(c)
+            if pending is not None:  # piece c-1's interleave behind piece c's encode
+                self._finish_gather(pending[1], pending[0], d_recovery)
+            pending = (c, work)
+        self._finish_gather(pending[1], pending[0], d_recovery)
 
 
 _sharded_cache: Dict[tuple, ShardedEncoder] = {}

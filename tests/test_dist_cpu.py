@@ -64,6 +64,39 @@ def _worker_sharded(rank, world, port, N, M, S, rate, q):
         dist.destroy_process_group()
 
 
+def _worker_pipelined(rank, world, port, N, M, S, chunks, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "reed-solomon-simd_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    import reed_solomon_simd as rs
+    _init(rank, world, port)
+    widths = []
+
+    def piece_standin(cols, out):
+        # CPU stand-in for the per-piece device encode (rs_encode_device_strided on a column piece)
+        widths.append(cols.shape[1])
+        out.copy_(torch.from_numpy(O.encode("high", np.ascontiguousarray(cols.numpy()), M)))
+
+    try:
+        orig = O.generate_original(N, S, 5 + chunks)
+        want = O.encode("high", orig, M)
+        enc = rs.ShardedEncoder(N, M, S, group=None, rate_=1, encode_slice=piece_standin, chunks=chunks)
+        ok = True
+        for _ in range(2):
+            d_rec = torch.zeros((M, S), dtype=torch.uint8)
+            enc(enc.columns(torch.from_numpy(orig)), d_rec)
+            ok = ok and bool(np.array_equal(d_rec.numpy(), want))
+        # the unpipelined path (one slice encode, then gather) gives the same matrix
+        enc.encode_local(enc.columns(torch.from_numpy(orig)))
+        d2 = torch.zeros((M, S), dtype=torch.uint8)
+        enc.gather(d2)
+        ok = ok and bool(np.array_equal(d2.numpy(), want))
+        q.put((rank, (ok, widths)))
+    finally:
+        dist.destroy_process_group()
+
+
 def _worker_reduce(rank, world, port, q):
     import sys
     sys.path.insert(0, ROOT)
@@ -94,6 +127,16 @@ def _spawn(fn, world, *args):
 def test_column_partitioned_encode(world, N, M, S, rate):
     out = _spawn(_worker_sharded, world, N, M, S, rate)
     assert out == {r: (True, 2, 1) for r in range(world)}
+
+
+@pytest.mark.parametrize("world,N,M,S,chunks", [(2, 64, 64, 512, 2), (2, 300, 200, 1024, 4), (4, 100, 100, 1024, 4),
+                                                (2, 64, 64, 256, 1)])
+def test_pipelined_column_partitioned_encode(world, N, M, S, chunks):
+    """ShardedEncoder in pieces: piece c's all-gather (async) overlaps piece c+1's encode and
+    piece c-1's interleave; every rank ends with the single-device recovery matrix."""
+    out = _spawn(_worker_pipelined, world, N, M, S, chunks)
+    w = S // world
+    assert out == {r: (True, [w // chunks] * (2 * chunks) + [w]) for r in range(world)}
 
 
 def test_bench_max_over_ranks_world2():
