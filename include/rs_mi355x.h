@@ -309,7 +309,10 @@ rs_status rs_check_device(rs_context *ctx);
  * decodes of at most 192 4-element packs use packs of 2 elements (twice the
  * workgroups; RS_MI355X_E2_MAX_PACKS sets the limit): adding 8 keeps 4-element
  * packs, adding 16 uses 2-element packs for every single-chunk launch, encodes
- * included.  A/B and tests; results are identical in every mode. */
+ * included.  Adding 32 runs one-chunk encodes of 2^9 .. 2^11 rows over at most
+ * 128 packs as two workgroups per pack with an in-launch hand-off (pair
+ * encode; also RS_MI355X_PAIR=1; measured no faster).  A/B and
+ * tests; results are identical in every mode. */
 rs_status rs_mono_enable(rs_context *ctx, int enable);
 
 /* ---- GF(2^16) tables (src/engine/tables.rs), host copies ---- */

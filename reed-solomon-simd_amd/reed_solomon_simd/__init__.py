@@ -143,7 +143,8 @@ _sig("rs_mono_enable", _int, _vp, _int)
 
 def mono_enable(enable=True, ctx=None) -> None:
     """Column kernel (one workgroup per pack): False = never, True = where fastest (default),
-    2 = also multi-chunk and 2^11 / 2^12-row transforms."""
+    2 = also multi-chunk and 2^11 / 2^12-row transforms; + 4 no split decode plan, + 8 4-element
+    packs only, + 16 2-element packs everywhere, + 32 pair encode (rs_mono_enable)."""
     ctx = ctx or default_context()
     _lib.rs_mono_enable(ctx.handle, int(enable))
 
