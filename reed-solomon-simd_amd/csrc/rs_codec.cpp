@@ -493,12 +493,11 @@ void launch_pair(rs_context *ctx, Workspace &ws, int mode, uint32_t L, const Geo
         Mo.top[q] = T.perm_by_skew[ii * rs::kPermWords + q] ^ T.perm_by_skew[fi * rs::kPermWords + q];
     // granules: 2 halves x 8 x packs_per_xcd pairs x threads x 4 (2 rows x 2 words)
     const size_t need = size_t(16) * Mo.packs_per_xcd * (size_t(1) << (Lh - 1)) * 4 * 8;
-    if (ws.xchg.cap < need) {
-        ws.xchg.get(need);
-        check(hipMemsetAsync(ws.xchg.p, 0, need, s));
-    }
+    bool zero = false;
+    if (ws.xchg.cap < need) ws.xchg.get(need), zero = true;
+    if (++ws.pair_epoch == 0) ws.pair_epoch = 1, zero = true;  // wrapped: old tags could match again
+    if (zero) check(hipMemsetAsync(ws.xchg.p, 0, ws.xchg.cap, s));
     Mo.xchg = static_cast<uint64_t *>(ws.xchg.p);
-    if (++ws.pair_epoch == 0) ws.pair_epoch = 1;  // (2^32 launches later) never 0
     Mo.epoch = ws.pair_epoch;
     Mo.pair_timeouts = ctx->d_pair_timeouts;
     hipEvent_t ev = nullptr;

@@ -664,18 +664,26 @@ __device__ __forceinline__ void scale_issue(const MonoArgs &A, const uint32_t *r
     static_for<0, (1 << LR)>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         const uint32_t f = rowinfo[a | reg_rows<S, 0, LR>(i)];
-        // rows that are not received read one shared dummy table (log 0):
-        // the gather costs cache lines only for the rows that use it
-        uint32_t lg = (f & 0x10000u) ? 0u : (f & 0xFFFFu);
+        uint32_t lg = f & 0xFFFFu;
 #ifdef RS_MONO_SKIP_SCALE  // tools/mono_probe.hip ablation: one shared table
         lg = 0;
 #endif
         st.erased |= ((f >> 16) & 1u) << i;
-        const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + lg * PC;
+#ifndef RS_MONO_SCALE_ALL_LANES
+        // only received rows gather a table (finish_col zeroes the others): lanes
+        // that load nothing return no bytes, so a 1 % decode's rows that are not
+        // received -- half the work rows -- cost no load bandwidth
+        if (!(f & 0x10000u))
+#else
+        if (f & 0x10000u) lg = 0;  // (the others read one shared table)
+#endif
+        {
+            const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + lg * PC;
 #pragma unroll
-        for (int v = 0; v < int(PC); ++v) {
-            const uint4 x = q[v];
-            st.t[i][4 * v] = x.x, st.t[i][4 * v + 1] = x.y, st.t[i][4 * v + 2] = x.z, st.t[i][4 * v + 3] = x.w;
+            for (int v = 0; v < int(PC); ++v) {
+                const uint4 x = q[v];
+                st.t[i][4 * v] = x.x, st.t[i][4 * v + 1] = x.y, st.t[i][4 * v + 2] = x.z, st.t[i][4 * v + 3] = x.w;
+            }
         }
     });
 }
@@ -1329,6 +1337,10 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
             RS_MSTAMP(2);
         }
         ScaleTabs<L, LR, E> st;
+        // (decodes) every load issued so far -- rows, tables, eval_poly's inputs --
+        // has landed while eval_poly ran; saying so here lets the table writes
+        // below go ahead without waiting for the (lane-conditional) scale gathers
+        if constexpr (DEC) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
         if constexpr (DEC) scale_issue<L, LR, SPLIT, E>(A, ri, st, lane, wave);
         auto write1 = [&]() {
 #ifndef RS_MONO_SKIP_STAGE
