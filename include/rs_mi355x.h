@@ -293,7 +293,8 @@ int rs_profile_collect(rs_context *ctx, float *ms, uint64_t *bytes, const char *
 /* ---- device check ----
  * rs_check_device synchronizes the context's device and returns
  * RS_ERR_DEVICE (message in rs_last_device_error) if an earlier asynchronous
- * launch failed, else RS_OK. */
+ * launch failed, or if a pair-encode workgroup (rs_mono_enable + 32) gave up
+ * waiting for its partner's half (its results are then invalid), else RS_OK. */
 rs_status rs_check_device(rs_context *ctx);
 
 /* ---- column kernel control (engine tuning, not a reference item) ----
