@@ -342,6 +342,17 @@ template <int L, int LR, bool SPLIT = false, int E = 4>
 struct Stage {
     static constexpr int TW = Fmt<E>::kTW;
     static constexpr uint32_t PC = Fmt<E>::kPC;
+    // LDS slot of a table: 20 words in both formats.  A 2-element table is 16
+    // words, and slots of 16 words (64 B, a quarter of the banks) would put lanes
+    // that read tables t and t + 4 on the same banks; 20-word slots cycle through
+    // all 16 four-bank groups (MI355X guide "LDS": ds_read_b128 lane groups)
+    static constexpr int SW = 20;
+    static constexpr uint32_t SPC = SW / 4;  // 16-byte pieces per slot
+    // LDS position (16-byte units) of piece q of a region's table sequence
+    static __device__ __forceinline__ uint32_t at(uint32_t q) {
+        if constexpr (SPC == PC) return q;
+        else return q + (q / PC) * (SPC - PC);
+    }
     static constexpr int IW = LR + 6, WB = L - IW - (SPLIT ? 1 : 0);
     static constexpr uint32_t n = 1u << L, W = 1u << IW;
     // layers of the last (FFT) in-wave phase
@@ -363,13 +374,13 @@ struct Stage {
     static constexpr uint32_t kShared = kShI + kShF;
     static constexpr uint32_t kWaves = 1u << (L - LR - 6);
     static constexpr uint32_t plane_words = (E == 4 ? 2 : 1) * n;
-    static constexpr uint32_t words = plane_words + (kShared + kWaves * kPriv) * TW;
+    static constexpr uint32_t words = plane_words + (kShared + kWaves * kPriv) * SW;
     // encode (IFFT and FFT on different skew offsets t_i, t_f): phase 3's tables
     // are phase 1's XOR D_b, one table per phase-3 layer b (twiddles are
     // GF(2)-linear in the global group index, so are the perm tables:
     // D_b = the table of group (t_i ^ t_f) * n / 2^(b+1)), kept after the shared tables
     static constexpr uint32_t kD = NB3;
-    static constexpr uint32_t words_enc = words + kD * TW;
+    static constexpr uint32_t words_enc = words + kD * SW;
     static constexpr uint32_t words_dec = words + n;  // + per-row decode info (fused eval_poly)
     // SPLIT decode: + a second column plane (the cross-half step's formal-derivative values)
     static constexpr uint32_t words_split = words_dec + (SPLIT ? plane_words : 0);
@@ -406,7 +417,7 @@ struct LdsTabs {
         for (int q = 0; q < G::TW; ++q) t[q] = slot * 0x01010101u + q + uint32_t(reinterpret_cast<uintptr_t>(base));
         return;
 #endif
-        const uint4 *p = reinterpret_cast<const uint4 *>(base) + slot * G::PC;
+        const uint4 *p = reinterpret_cast<const uint4 *>(base) + slot * G::SPC;
 #pragma unroll
         for (int q = 0; q < int(G::PC); ++q) {
             const uint4 v = p[q];
@@ -1260,7 +1271,7 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
         constexpr bool DEC = MODE == kMonoDecode;
         uint32_t *shared = lds + G::plane_words;
         constexpr uint32_t kSh = DEC ? G::kShared : G::kShared + G::kD;  // shared tables (+ D)
-        uint32_t *priv = shared + kSh * G::TW + wave * G::kPriv * G::TW;
+        uint32_t *priv = shared + kSh * G::SW + wave * G::kPriv * G::SW;
         uint32_t *rinfo = lds + G::words;  // decode with fused eval_poly
         constexpr uint32_t PC = G::PC;  // 16-byte pieces per table
         constexpr int KP1 = (PC * G::kUp + 63) / 64;
@@ -1346,7 +1357,7 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
 #ifndef RS_MONO_SKIP_STAGE
             static_for<0, KP1>([&](auto kc) {
                 const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < PC * G::kUp) reinterpret_cast<uint4 *>(priv)[q] = v1[kc];
+                if (q < PC * G::kUp) reinterpret_cast<uint4 *>(priv)[G::at(q)] = v1[kc];
             });
 #endif
         };
@@ -1354,13 +1365,13 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
         if constexpr (G::B0)
             static_for<0, KP0>([&](auto kc) {
                 const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[q] = v0[kc];
+                if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at(q)] = v0[kc];
             });
         else
             write1();
         static_for<0, KSH>([&](auto kc) {
             const uint32_t q = threadIdx.x + T * decltype(kc)::value;
-            if (q < PC * kSh) reinterpret_cast<uint4 *>(shared)[q] = vs[kc];
+            if (q < PC * kSh) reinterpret_cast<uint4 *>(shared)[G::at(q)] = vs[kc];
         });
 #endif
         RS_MSTAMP(6);
@@ -1386,21 +1397,21 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
                         const uint32_t q = lane + 64u * decltype(kc)::value;
                         if (q < PC * G::kP3) {
                             const uint32_t t = q / PC, piece = q - t * PC;
-                            const uint4 v = reinterpret_cast<const uint4 *>(priv)[q];
-                            const uint4 d = reinterpret_cast<const uint4 *>(shared)[(G::kShared + priv_layer<L, LR, SPLIT, E>(t)) * PC + piece];
+                            const uint4 v = reinterpret_cast<const uint4 *>(priv)[G::at(q)];
+                            const uint4 d = reinterpret_cast<const uint4 *>(shared)[(G::kShared + priv_layer<L, LR, SPLIT, E>(t)) * G::SPC + piece];
                             x[kc] = uint4{v.x ^ d.x, v.y ^ d.y, v.z ^ d.z, v.w ^ d.w};
                         }
                     });
                     static_for<0, KP3>([&](auto kc) {
                         const uint32_t q = lane + 64u * decltype(kc)::value;
-                        if (q < PC * G::kP3) reinterpret_cast<uint4 *>(priv)[q] = x[kc];
+                        if (q < PC * G::kP3) reinterpret_cast<uint4 *>(priv)[G::at(q)] = x[kc];
                     });
                 }
                 return;
             }
             static_for<0, KP3>([&](auto kc) {
                 const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < PC * G::kP3) reinterpret_cast<uint4 *>(priv)[q] = v3[kc];
+                if (q < PC * G::kP3) reinterpret_cast<uint4 *>(priv)[G::at(q)] = v3[kc];
             });
         };
         // B0: the FFT's layer-0 tables (phase 3's last layer), requested while the
@@ -1417,7 +1428,7 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
             if constexpr (G::B0)
                 static_for<0, KP0>([&](auto kc) {
                     const uint32_t q = lane + 64u * decltype(kc)::value;
-                    if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[q] = v4[kc];
+                    if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at(q)] = v4[kc];
                 });
         };
         if constexpr (SPLIT) {
@@ -1435,7 +1446,7 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
             const bool out = out_wave;
             const bool alive = out && wave_stores<L, LR, true>(A, wave);
             constexpr uint32_t kTopI = (G::n >> G::IW) - 2, kTopF = G::kShI + (G::n >> G::WB) - 2;
-            split_top<L, LR>(c, plane, lds + G::words_dec, shared + kTopI * G::TW, shared + kTopF * G::TW, lane, wave,
+            split_top<L, LR>(c, plane, lds + G::words_dec, shared + kTopI * G::SW, shared + kTopF * G::SW, lane, wave,
                              A.out_half);
             issue4(alive);
             // FFT below the top layer: only the half that holds restored rows
