@@ -1123,28 +1123,27 @@ __device__ __forceinline__ void col_walsh(uint32_t (&x)[2], uint32_t *buf) {
         constexpr int j = 7 + 2 * rnd;  // row bits j (and j + 1) = layers j (and j + 1)
         constexpr bool two = j + 1 < L;
         constexpr uint32_t h1 = 1u << (j - 1), h2 = two ? 1u << j : 0u;  // thread bits
-        uint32_t *b = buf + ((rnd & 1) << L);
-        b[2 * t] = x[0];
-        b[2 * t + 1] = x[1];
+        // a thread's two values as one 8-byte word: ds_write_b64 / ds_read_b64 of
+        // consecutive threads are conflict-free (stride-2 32-bit accesses were 2-way)
+        uint2 *b = reinterpret_cast<uint2 *>(buf + ((rnd & 1) << L));
+        b[t] = uint2{x[0], x[1]};
         __syncthreads();
         const uint32_t m1 = (t & h1) ? ~0u : 0u, c1 = m1 & kWalshM1<j>;
-        static_for<0, 2>([&](auto kc) {
-            constexpr int q = decltype(kc)::value;
-            if constexpr (!two) {
-                const uint32_t y = b[2 * (t ^ h1) + q];
-                x[q] = y + (x[q] ^ m1) + c1;
-            } else {
-                // v[b2][b1] of the group; this thread is (u2, u1)
-                const uint32_t m2 = (t & h2) ? ~0u : 0u, c2 = m2 & kWalshM1<j + 1>;
-                const uint32_t g0 = t & ~(h1 | h2);
-                const uint32_t v00 = b[2 * g0 + q], v01 = b[2 * (g0 | h1) + q];
-                const uint32_t v10 = b[2 * (g0 | h2) + q], v11 = b[2 * (g0 | h1 | h2) + q];
-                // layer j: own-role element of each pair (v?0 lower, v?1 upper)
-                const uint32_t lo = v00 + (v01 ^ m1) + c1;
-                const uint32_t hi = v10 + (v11 ^ m1) + c1;
-                x[q] = lo + (hi ^ m2) + c2;  // layer j + 1
-            }
-        });
+        if constexpr (!two) {
+            const uint2 y = b[t ^ h1];
+            x[0] = y.x + (x[0] ^ m1) + c1;
+            x[1] = y.y + (x[1] ^ m1) + c1;
+        } else {
+            // v[b2][b1] of the group; this thread is (u2, u1)
+            const uint32_t m2 = (t & h2) ? ~0u : 0u, c2 = m2 & kWalshM1<j + 1>;
+            const uint32_t g0 = t & ~(h1 | h2);
+            const uint2 v00 = b[g0], v01 = b[g0 | h1], v10 = b[g0 | h2], v11 = b[g0 | h1 | h2];
+            // layer j: own-role element of each pair (v?0 lower, v?1 upper)
+            const uint32_t lo0 = v00.x + (v01.x ^ m1) + c1, lo1 = v00.y + (v01.y ^ m1) + c1;
+            const uint32_t hi0 = v10.x + (v11.x ^ m1) + c1, hi1 = v10.y + (v11.y ^ m1) + c1;
+            x[0] = lo0 + (hi0 ^ m2) + c2;  // layer j + 1
+            x[1] = lo1 + (hi1 ^ m2) + c2;
+        }
     });
     x[0] = walsh_fold(x[0]);
     x[1] = walsh_fold(x[1]);
@@ -1174,10 +1173,8 @@ __device__ __forceinline__ void col_eval_poly(const MonoArgs &A, uint32_t ebits,
     });
     if constexpr (L > 7) __syncthreads();  // the first transform's last LDS reads are done
     col_walsh<L>(x, buf);
-    static_for<0, 2>([&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        rinfo[i0 + k] = x[k] | (((rbits >> k) & 1u) ? 0u : 0x10000u);
-    });
+    reinterpret_cast<uint2 *>(rinfo)[threadIdx.x] =
+        uint2{x[0] | ((rbits & 1u) ? 0u : 0x10000u), x[1] | ((rbits & 2u) ? 0u : 0x10000u)};
     __syncthreads();
 }
 
