@@ -348,10 +348,42 @@ struct Stage {
     // all 16 four-bank groups (MI355X guide "LDS": ds_read_b128 lane groups)
     static constexpr int SW = 20;
     static constexpr uint32_t SPC = SW / 4;  // 16-byte pieces per slot
-    // LDS position (16-byte units) of piece q of a region's table sequence
-    static __device__ __forceinline__ uint32_t at(uint32_t q) {
-        if constexpr (SPC == PC) return q;
-        else return q + (q / PC) * (SPC - PC);
+    // Within a layer, group g's table sits at slot sg(g) = g ^ ((g >> 1) & 15) of the
+    // layer's range.  The plan puts row bits 3 and 4 (and, in the FFT's top phase,
+    // similar pairs) on lane bits of one ds_read_b128 lane group, so layers 0 and 1
+    // read groups 2 and 4 slots apart on the same banks; the Gray-code swizzle
+    // spreads them (a model of every table read of the plans, tools/lds_bank_model.py,
+    // gives conflict-free reads for L = 8..11).  Measured (profiles/r02h/ab_gray): the
+    // 2-element decode's conflict cycles 708K -> 566K per launch and -0.2 us, but the
+    // 4-element encode's 106K -> 204K (the permuted staging writes and the phase-3 XOR
+    // pass conflict instead) and +0.2 us, so only the 2-element format uses it
+    static constexpr bool kGray = E == 2;
+    static __device__ __forceinline__ uint32_t sg(uint32_t g) { return kGray ? g ^ ((g >> 1) & 15u) : g; }
+    // slot of table t of a region sequence of 2^k - 1 tables, layers largest first
+    // (layer of size 2^m starts at 2^k - 2^(m+1), a multiple of 2^m)
+    static __device__ __forceinline__ uint32_t sq(uint32_t t, uint32_t k) {
+        if constexpr (!kGray) return t;
+        const uint32_t y = (1u << k) - t;  // 2^m < y <= 2^(m+1)
+        const uint32_t mask = y <= 1u ? 0u : (1u << (31 - __builtin_clz(y - 1u))) - 1u;
+        return t ^ (((t & mask) >> 1) & 15u);
+    }
+    // LDS position (16-byte units) of piece q of table slot (q / PC) -> f(q / PC)
+    template <typename F>
+    static __device__ __forceinline__ uint32_t at(uint32_t q, F f) {
+        const uint32_t t = q / PC;
+        return f(t) * SPC + (q - t * PC);
+    }
+    // the phase-1 / -3 region (layers B0..IW-1), its layer-0 turn (B0), the shared region
+    static __device__ __forceinline__ uint32_t at1(uint32_t q) {
+        return at(q, [](uint32_t t) { return sq(t, uint32_t(IW - B0)); });
+    }
+    static __device__ __forceinline__ uint32_t at0(uint32_t q) { return at(q, [](uint32_t t) { return sg(t); }); }
+    static __device__ __forceinline__ uint32_t atS(uint32_t q) {
+        return at(q, [](uint32_t t) {
+            if (t < kShI) return sq(t, uint32_t(L - IW));
+            if (t < kShI + kShF) return kShI + sq(t - kShI, uint32_t(L - WB));
+            return t;  // D tables: one per layer
+        });
     }
     static constexpr int IW = LR + 6, WB = L - IW - (SPLIT ? 1 : 0);
     static constexpr uint32_t n = 1u << L, W = 1u << IW;
@@ -401,16 +433,16 @@ struct LdsTabs {
         uint32_t slot;
         const uint32_t *base;
         if constexpr ((PH == 1 || PH == 3) && G::B0 == 1 && S::v.ops[I].bit == 0) {
-            slot = (row & (G::W - 1)) >> 1;  // layer 0's turn in the region
+            slot = G::sg((row & (G::W - 1)) >> 1);  // layer 0's turn in the region
             base = priv;
         } else if constexpr (PH == 1 || PH == 3) {
-            slot = (G::W >> G::B0) - (G::W >> x) + ((row & (G::W - 1)) >> (x + 1));
+            slot = (G::W >> G::B0) - (G::W >> x) + G::sg((row & (G::W - 1)) >> (x + 1));
             base = priv;
         } else if constexpr (PH == 2) {
-            slot = (G::n >> G::IW) - (G::n >> x) + (row >> (x + 1));
+            slot = (G::n >> G::IW) - (G::n >> x) + G::sg(row >> (x + 1));
             base = shared;
         } else {
-            slot = G::kShI + (G::n >> G::WB) - (G::n >> x) + (row >> (x + 1));
+            slot = G::kShI + (G::n >> G::WB) - (G::n >> x) + G::sg(row >> (x + 1));
             base = shared;
         }
 #ifdef RS_MONO_FAKE_TABS  // tools/mono_probe.hip: tables without LDS traffic
@@ -1354,7 +1386,7 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
 #ifndef RS_MONO_SKIP_STAGE
             static_for<0, KP1>([&](auto kc) {
                 const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < PC * G::kUp) reinterpret_cast<uint4 *>(priv)[G::at(q)] = v1[kc];
+                if (q < PC * G::kUp) reinterpret_cast<uint4 *>(priv)[G::at1(q)] = v1[kc];
             });
 #endif
         };
@@ -1362,13 +1394,13 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
         if constexpr (G::B0)
             static_for<0, KP0>([&](auto kc) {
                 const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at(q)] = v0[kc];
+                if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at0(q)] = v0[kc];
             });
         else
             write1();
         static_for<0, KSH>([&](auto kc) {
             const uint32_t q = threadIdx.x + T * decltype(kc)::value;
-            if (q < PC * kSh) reinterpret_cast<uint4 *>(shared)[G::at(q)] = vs[kc];
+            if (q < PC * kSh) reinterpret_cast<uint4 *>(shared)[G::atS(q)] = vs[kc];
         });
 #endif
         RS_MSTAMP(6);
@@ -1394,21 +1426,21 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
                         const uint32_t q = lane + 64u * decltype(kc)::value;
                         if (q < PC * G::kP3) {
                             const uint32_t t = q / PC, piece = q - t * PC;
-                            const uint4 v = reinterpret_cast<const uint4 *>(priv)[G::at(q)];
+                            const uint4 v = reinterpret_cast<const uint4 *>(priv)[G::at1(q)];
                             const uint4 d = reinterpret_cast<const uint4 *>(shared)[(G::kShared + priv_layer<L, LR, SPLIT, E>(t)) * G::SPC + piece];
                             x[kc] = uint4{v.x ^ d.x, v.y ^ d.y, v.z ^ d.z, v.w ^ d.w};
                         }
                     });
                     static_for<0, KP3>([&](auto kc) {
                         const uint32_t q = lane + 64u * decltype(kc)::value;
-                        if (q < PC * G::kP3) reinterpret_cast<uint4 *>(priv)[G::at(q)] = x[kc];
+                        if (q < PC * G::kP3) reinterpret_cast<uint4 *>(priv)[G::at1(q)] = x[kc];
                     });
                 }
                 return;
             }
             static_for<0, KP3>([&](auto kc) {
                 const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < PC * G::kP3) reinterpret_cast<uint4 *>(priv)[G::at(q)] = v3[kc];
+                if (q < PC * G::kP3) reinterpret_cast<uint4 *>(priv)[G::at1(q)] = v3[kc];
             });
         };
         // B0: the FFT's layer-0 tables (phase 3's last layer), requested while the
@@ -1425,7 +1457,7 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
             if constexpr (G::B0)
                 static_for<0, KP0>([&](auto kc) {
                     const uint32_t q = lane + 64u * decltype(kc)::value;
-                    if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at(q)] = v4[kc];
+                    if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at0(q)] = v4[kc];
                 });
         };
         if constexpr (SPLIT) {
