@@ -437,8 +437,10 @@ bool use_mono(rs_context *ctx, uint32_t L, const Geom &g, uint32_t chunks) {
 
 // Staged decodes of few packs use 2-element packs: twice the workgroups on
 // a chip whose CUs the 4-element packs leave idle (rs_mono.hip Fmt).  The
-// headline encode measured slower that way (9.4 vs 8.4 us per launch), the
-// decode faster (14.6 vs 15.4 us), hence decodes only by default.
+// headline encode measured slower that way (9.4 vs 8.4 us per launch; after the
+// 20-word LDS slots and the slot swizzle of the 2-element tables about equal,
+// 8.5-8.8 vs 8.4-8.75 us), the decode faster (14.6 vs 15.4 us, now 13.8), hence
+// decodes only by default.
 rs::MonoArgs mono_args(rs_context *ctx, uint32_t L, const Geom &g, bool staged, bool decode = false) {
     rs::MonoArgs M;
     const bool e2 = staged && (decode || ctx->e2_encode) && g.packs <= ctx->e2_max_packs && L <= 11;
