@@ -37,7 +37,12 @@
  * host by an internal mutex, and the device scratch is kept per (context,
  * stream), so calls enqueued on different streams may execute concurrently on
  * the device.  Do not destroy a stream while calls on it are in flight and
- * then pass a new stream that reuses its handle.  Every entry point runs on
+ * then pass a new stream that reuses its handle.  A context keeps the scratch
+ * of at most RS_MAX_STREAM_WORKSPACES streams (device buffers sized to the
+ * largest call made on each, plus pinned staging); a call on a further stream
+ * first synchronizes the device and frees the least recently used stream's
+ * scratch.  rs_release_stream_scratch frees one stream's scratch at once (call
+ * it before destroying a stream the context has seen).  Every entry point runs on
  * the context's device and restores the calling thread's current device.  An
  * encoder/decoder handle is used by one thread at a time (like
  * &mut ReedSolomonEncoder).
@@ -135,7 +140,9 @@ int rs_encoder_is_high_rate(const rs_encoder *enc);
 void rs_encoder_free(rs_encoder *enc);
 /* RateEncoder::into_parts (src/rate.rs:129-131): consumes enc (freed), returns its engine
  * (the context) and its working space (host and device buffers) for reuse by another
- * encoder of any rate and shape.  Either out pointer may be NULL. */
+ * encoder of any rate and shape.  Either out pointer may be NULL.  The work remembers
+ * the device of the context it came from: handed to a context on another device, its
+ * device buffers are freed (not reused) and only its host buffers are kept. */
 rs_status rs_encoder_into_parts(rs_encoder *enc, rs_context **ctx_out, rs_encoder_work **work_out);
 /* RateEncoder::new with `work: Option<EncoderWork>` (src/rate.rs:133-139,
  * src/rate/rate_high.rs:93-103): like
@@ -280,6 +287,11 @@ rs_status rs_engine_ifft_host(rs_context *ctx, uint8_t *rows, uint64_t shard_cou
                               uint64_t pos, uint64_t size, uint64_t truncated_size, uint64_t skew_delta);
 rs_status rs_engine_mul_host(rs_context *ctx, uint8_t *blocks, uint64_t block_count, uint16_t log_m);
 
+/* Device scratch of one stream (see "Thread-safety"): synchronizes `stream`
+ * and frees the context's scratch for it.  The stream must still be valid. */
+#define RS_MAX_STREAM_WORKSPACES 16
+rs_status rs_release_stream_scratch(rs_context *ctx, void *stream);
+
 /* ---- kernel timing (bench instrumentation, not a reference item) ----
  * While enabled, every kernel the context launches is bracketed by HIP events
  * on the stream it is launched on.  rs_profile_collect synchronizes those
@@ -293,8 +305,7 @@ int rs_profile_collect(rs_context *ctx, float *ms, uint64_t *bytes, const char *
 /* ---- device check ----
  * rs_check_device synchronizes the context's device and returns
  * RS_ERR_DEVICE (message in rs_last_device_error) if an earlier asynchronous
- * launch failed, or if a pair-encode workgroup (rs_mono_enable + 32) gave up
- * waiting for its partner's half (its results are then invalid), else RS_OK. */
+ * launch failed, else RS_OK. */
 rs_status rs_check_device(rs_context *ctx);
 
 /* ---- column kernel control (engine tuning, not a reference item) ----
@@ -310,10 +321,7 @@ rs_status rs_check_device(rs_context *ctx);
  * decodes of at most 192 4-element packs use packs of 2 elements (twice the
  * workgroups; RS_MI355X_E2_MAX_PACKS sets the limit): adding 8 keeps 4-element
  * packs, adding 16 uses 2-element packs for every single-chunk launch, encodes
- * included.  Adding 32 runs one-chunk encodes of 2^9 .. 2^11 rows over at most
- * 128 packs as two workgroups per pack with an in-launch hand-off (pair
- * encode; also RS_MI355X_PAIR=1; measured no faster).  A/B and
- * tests; results are identical in every mode. */
+ * included.  A/B and tests; results are identical in every mode. */
 rs_status rs_mono_enable(rs_context *ctx, int enable);
 
 /* ---- GF(2^16) tables (src/engine/tables.rs), host copies ---- */

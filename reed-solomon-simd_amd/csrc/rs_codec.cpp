@@ -155,19 +155,12 @@ struct Workspace {
     DevBuf buf[4], rowinfo, state;
     std::vector<uint8_t> h_state;
     PinnedBuf h_state_pinned;  // source of the erasure-state copy of large decodes
-    // pair encode hand-off granules (rs_mono.hip pair_top): zeroed once when
-    // allocated; every pair launch on this stream tags its granules with the
-    // next epoch, so granules of earlier launches never match
-    DevBuf xchg;
-    uint32_t pair_epoch = 0;
     void swap(Workspace &o) {
         for (int k = 0; k < 4; ++k) buf[k].swap(o.buf[k]);
         rowinfo.swap(o.rowinfo);
         state.swap(o.state);
         h_state.swap(o.h_state);
         h_state_pinned.swap(o.h_state_pinned);
-        xchg.swap(o.xchg);
-        std::swap(pair_epoch, o.pair_epoch);
     }
 };
 
@@ -207,25 +200,35 @@ struct rs_context {
     uint32_t e2_max_packs = 192;
     bool e2_encode = false;
     uint32_t *d_lut2 = nullptr;   // perm2_by_log: the 2-element form of d_lut
-    // pair encode (rs_mono.hip pair_top): one-chunk encodes of 2^9 .. 2^11 rows over
-    // at most pair_max_packs packs as two workgroups per pack.  Off by default:
-    // measured no faster at the headline (k_mono_pair<9> 8.71 us vs k_mono<10>
-    // 8.68 us per launch, profiles/r02g/ab_pair: the in-launch hand-off costs what
-    // the halved workgroups save).  RS_MI355X_PAIR=1 / rs_mono_enable + 32 turn it on.
-    bool pair = false;
-    uint32_t pair_max_packs = 128;
-    uint32_t *d_pair_timeouts = nullptr;  // bounded-spin give-ups of the pair kernel (must stay 0)
     std::mutex img_mu;            // guards d_img, d_img2
     uint32_t *d_img[13] = {};     // column-kernel twiddle images per L (built at context creation)
     uint32_t *d_img2[13] = {};    // the same in the 2-element table format
     std::mutex host_engine_mu;  // guards host_engine_buf (rs_engine_*_host staging)
     DevBuf host_engine_buf;
     std::mutex mu;  // guards ws_by_stream (device-resident API scratch), prof, recs
-    std::unordered_map<hipStream_t, std::unique_ptr<Workspace>> ws_by_stream;
-    Workspace &ws(hipStream_t s) {  // caller holds mu
-        auto &w = ws_by_stream[s];
-        if (!w) w.reset(new Workspace);
-        return *w;
+    // at most RS_MAX_STREAM_WORKSPACES entries; the least recently used one is
+    // evicted (after a device synchronize: its stream may still use it, and the
+    // stream itself may already be destroyed) when a further stream arrives
+    struct WsEntry {
+        std::unique_ptr<Workspace> w;
+        uint64_t last_use = 0;
+    };
+    std::unordered_map<hipStream_t, WsEntry> ws_by_stream;
+    uint64_t ws_clock = 0;
+    Workspace &ws(hipStream_t s) {  // caller holds mu, on the context's device
+        auto it = ws_by_stream.find(s);
+        if (it == ws_by_stream.end()) {
+            if (ws_by_stream.size() >= RS_MAX_STREAM_WORKSPACES) {
+                auto lru = ws_by_stream.begin();
+                for (auto j = ws_by_stream.begin(); j != ws_by_stream.end(); ++j)
+                    if (j->second.last_use < lru->second.last_use) lru = j;
+                check(hipDeviceSynchronize());
+                ws_by_stream.erase(lru);
+            }
+            it = ws_by_stream.emplace(s, WsEntry{std::unique_ptr<Workspace>(new Workspace), 0}).first;
+        }
+        it->second.last_use = ++ws_clock;
+        return *it->second.w;
     }
     // kernel timing (rs_profile_enable)
     // host-memory pipeline (rs_encode_host / rs_decode_host), built on first use
@@ -464,50 +467,6 @@ void launch_mono(int mode, uint32_t L, const rs::MonoArgs &M, hipStream_t s, uin
     if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), bytes);
 }
 
-// Pair encode (rs_mono.hip pair_top, MonoArgs "Pair encode"): a one-chunk,
-// one-stripe encode of 2^L rows over few packs -- whose one workgroup per pack
-// would leave CUs idle -- runs as two workgroups per pack, one per half of
-// the rows.  Not inside a stream capture: a replayed graph would reuse the
-// launch's hand-off epoch.
-bool use_pair(rs_context *ctx, uint32_t L, const Geom &g, uint32_t chunks, hipStream_t s) {
-    if (!ctx->pair || !ctx->mono || ctx->e2_encode || chunks != 1 || g.stripes != 1) return false;
-    if (g.packs > ctx->pair_max_packs || int(L) - 1 < rs::kMonoPairMinL || int(L) - 1 > rs::kMonoPairMaxL) return false;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    check(hipStreamIsCapturing(s, &cs));
-    return cs == hipStreamCaptureStatusNone;
-}
-
-// ti / tf: skew offsets of the IFFT / FFT in units of n = 2^L.
-void launch_pair(rs_context *ctx, Workspace &ws, int mode, uint32_t L, const Geom &g, rs::MonoArgs Mo, uint32_t ti,
-                 uint32_t tf, hipStream_t s, uint64_t bytes) {
-    const uint32_t Lh = L - 1;  // rows per workgroup: 2^Lh
-    const rs::MonoArgs base = mono_args(ctx, Lh, g, true);
-    Mo.img = base.img;
-    Mo.img_words = base.img_words;
-    Mo.ifft_img = 2 * ti;
-    Mo.fft_img = 2 * tf;
-    // table of mI + mF, the two top-layer twiddles (layer L-1, group 0: skew index
-    // 2^(L-1) + t * 2^L - 1)
-    const rs::GfTables &T = rs::tables();
-    const size_t ii = (size_t(1) << (L - 1)) + size_t(ti) * (size_t(1) << L) - 1;
-    const size_t fi = (size_t(1) << (L - 1)) + size_t(tf) * (size_t(1) << L) - 1;
-    for (int q = 0; q < int(rs::kPermWords); ++q)
-        Mo.top[q] = T.perm_by_skew[ii * rs::kPermWords + q] ^ T.perm_by_skew[fi * rs::kPermWords + q];
-    // granules: 2 halves x 8 x packs_per_xcd pairs x threads x 4 (2 rows x 2 words)
-    const size_t need = size_t(16) * Mo.packs_per_xcd * (size_t(1) << (Lh - 1)) * 4 * 8;
-    bool zero = false;
-    if (ws.xchg.cap < need) ws.xchg.get(need), zero = true;
-    if (++ws.pair_epoch == 0) ws.pair_epoch = 1, zero = true;  // wrapped: old tags could match again
-    if (zero) check(hipMemsetAsync(ws.xchg.p, 0, ws.xchg.cap, s));
-    Mo.xchg = static_cast<uint64_t *>(ws.xchg.p);
-    Mo.epoch = ws.pair_epoch;
-    Mo.pair_timeouts = ctx->d_pair_timeouts;
-    hipEvent_t ev = nullptr;
-    if (t_prof_ctx) prof_begin(s, &ev);
-    check(rs::launch_mono_pair(mode, int(Lh), Mo, s));
-    if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), bytes);
-}
-
 // HighRate encode (rate_high.rs:44-87) from device rows to device rows:
 // chunk c's IFFT uses skew_delta c*n + n, the chunks are XOR-folded, one FFT
 // with skew_delta 0 produces the recovery rows.
@@ -538,10 +497,6 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
         Mo.ifft_img = 1;  // chunk c: skew offset c * n + n
         Mo.ifft_img_step = 1;
         Mo.fft_img = 0;
-        if (use_pair(ctx, L, g, C, s)) {
-            launch_pair(ctx, ws, rs::kMonoEncodeHigh, L, g, Mo, 1, 0, s, (N + M) * uint64_t(g.packs) * 8);
-            return;
-        }
         launch_mono(rs::kMonoEncodeHigh, L, Mo, s, (N + M) * uint64_t(g.packs) * 8 * g.stripes);
         return;
     }
@@ -606,10 +561,6 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
         Mo.ifft_img = 0;
         Mo.fft_img = 1;  // output chunk c: skew offset c * n + n
         Mo.fft_img_step = 1;
-        if (use_pair(ctx, L, g, C, s)) {
-            launch_pair(ctx, ws, rs::kMonoEncodeLow, L, g, Mo, 0, 1, s, (N + M) * uint64_t(g.packs) * 8);
-            return;
-        }
         launch_mono(rs::kMonoEncodeLow, L, Mo, s, (N + M) * uint64_t(g.packs) * 8 * g.stripes);
         return;
     }
@@ -977,28 +928,41 @@ struct rs_decoder {
 
 // EncoderWork / DecoderWork (src/rate.rs:129-131, 206-208): an encoder's or
 // decoder's buffers, handed from one object to the next (any rate, any shape).
+// EncoderWork / DecoderWork: the buffers of an encoder / decoder handed from one
+// object to the next (rate.rs:129-139).  The device buffers (and the pinned
+// staging's event) belong to the device of the context that made them
+// (`device`): swap_host moves only the host buffers, for a context on another
+// device (device memory of GPU0 must not back GPU1's kernels).
 struct rs_encoder_work {
+    int device = -1;
     std::vector<uint8_t> h_orig, h_rec;
     DevBuf d_orig, d_rec;
     Workspace ws;
-    void swap(rs_encoder &e) {
+    void swap_host(rs_encoder &e) {
         h_orig.swap(e.h_orig);
         h_rec.swap(e.h_rec);
+    }
+    void swap(rs_encoder &e) {
+        swap_host(e);
         d_orig.swap(e.d_orig);
         d_rec.swap(e.d_rec);
         ws.swap(e.ws);
     }
 };
 struct rs_decoder_work {
+    int device = -1;
     std::vector<uint8_t> orig_present, rec_present, h_orig, h_rec, h_out;
     DevBuf d_orig, d_rec, d_out;
     Workspace ws;
-    void swap(rs_decoder &d) {
+    void swap_host(rs_decoder &d) {
         orig_present.swap(d.orig_present);
         rec_present.swap(d.rec_present);
         h_orig.swap(d.h_orig);
         h_rec.swap(d.h_rec);
         h_out.swap(d.h_out);
+    }
+    void swap(rs_decoder &d) {
+        swap_host(d);
         d_orig.swap(d.d_orig);
         d_rec.swap(d.d_rec);
         d_out.swap(d.d_out);
@@ -1107,10 +1071,6 @@ rs_status rs_context_create(int device, rs_context **out) {
         check(hipMemcpy(ctx->d_lwfold, T.lw_fold.data(), T.lw_fold.size() * 2, hipMemcpyHostToDevice));
         check(hipMalloc(&ctx->d_lut2, T.perm2_by_log.size() * 4));
         check(hipMemcpy(ctx->d_lut2, T.perm2_by_log.data(), T.perm2_by_log.size() * 4, hipMemcpyHostToDevice));
-        check(hipMalloc(&ctx->d_pair_timeouts, 4));
-        check(hipMemset(ctx->d_pair_timeouts, 0, 4));
-        const char *np = getenv("RS_MI355X_PAIR");
-        ctx->pair = np && np[0] == '1';
         ctx->lw0 = T.log_walsh[0];
         const char *nm = getenv("RS_MI355X_NO_MONO");
         ctx->mono = !(nm && nm[0] == '1');
@@ -1145,7 +1105,6 @@ void rs_context_destroy(rs_context *ctx) {
     if (ctx->d_tw) (void)hipFree(ctx->d_tw);
     if (ctx->d_lut) (void)hipFree(ctx->d_lut);
     if (ctx->d_lut2) (void)hipFree(ctx->d_lut2);
-    if (ctx->d_pair_timeouts) (void)hipFree(ctx->d_pair_timeouts);
     for (uint32_t *p : ctx->d_img2)
         if (p) (void)hipFree(p);
     if (ctx->d_lwfold) (void)hipFree(ctx->d_lwfold);
@@ -1479,7 +1438,10 @@ rs_status rs_encoder_new_with_work(rs_context *ctx, rs_rate rate, uint64_t N, ui
     auto *e = new rs_encoder;
     e->ctx = ctx;
     e->rate = rate;
-    if (w) w->swap(*e);
+    if (w) {
+        if (w->device == ctx->device) w->swap(*e);
+        else w->swap_host(*e);  // device buffers of another device: freed with w
+    }
     const rs_status st = encoder_configure(e, N, M, S, err);
     if (st != RS_OK) {
         delete e;
@@ -1552,6 +1514,7 @@ void rs_encoder_free(rs_encoder *e) { delete e; }
 rs_status rs_encoder_into_parts(rs_encoder *e, rs_context **ctx_out, rs_encoder_work **work_out) {
     if (!e) return RS_ERR_INVALID_ARGUMENT;
     auto *w = new rs_encoder_work;
+    w->device = e->ctx->device;
     w->swap(*e);
     if (ctx_out) *ctx_out = e->ctx;
     if (work_out) *work_out = w;
@@ -1577,7 +1540,10 @@ rs_status rs_decoder_new_with_work(rs_context *ctx, rs_rate rate, uint64_t N, ui
     auto *d = new rs_decoder;
     d->ctx = ctx;
     d->rate = rate;
-    if (w) w->swap(*d);
+    if (w) {
+        if (w->device == ctx->device) w->swap(*d);
+        else w->swap_host(*d);  // device buffers of another device: freed with w
+    }
     const rs_status st = decoder_configure(d, N, M, S, err);
     if (st != RS_OK) {
         delete d;
@@ -1685,6 +1651,7 @@ void rs_decoder_free(rs_decoder *d) { delete d; }
 rs_status rs_decoder_into_parts(rs_decoder *d, rs_context **ctx_out, rs_decoder_work **work_out) {
     if (!d) return RS_ERR_INVALID_ARGUMENT;
     auto *w = new rs_decoder_work;
+    w->device = d->ctx->device;
     w->swap(*d);
     if (ctx_out) *ctx_out = d->ctx;
     if (work_out) *work_out = w;
@@ -1885,6 +1852,20 @@ rs_status rs_engine_mul_host(rs_context *ctx, uint8_t *blocks, uint64_t block_co
     });
 }
 
+rs_status rs_release_stream_scratch(rs_context *ctx, void *stream) {
+    if (!ctx) return RS_ERR_INVALID_ARGUMENT;
+    return guarded(nullptr, [&]() -> rs_status {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        DeviceGuard dg(ctx->device);
+        auto s = static_cast<hipStream_t>(stream);
+        auto it = ctx->ws_by_stream.find(s);
+        if (it == ctx->ws_by_stream.end()) return RS_OK;
+        check(hipStreamSynchronize(s));
+        ctx->ws_by_stream.erase(it);
+        return RS_OK;
+    });
+}
+
 rs_status rs_profile_enable(rs_context *ctx, int enable) {
     if (!ctx) return RS_ERR_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> lock(ctx->mu);
@@ -1901,7 +1882,6 @@ rs_status rs_mono_enable(rs_context *ctx, int enable) {
     // + 8: 4-element packs only; + 16: 2-element packs wherever the staged kernel runs
     ctx->e2_max_packs = (enable & 8) ? 0u : (enable & 16) ? 0xFFFFFFFFu : 192u;
     ctx->e2_encode = (enable & 16) != 0;
-    ctx->pair = (enable & 32) != 0;  // + 32: pair encode
     return RS_OK;
 }
 
@@ -1911,13 +1891,6 @@ rs_status rs_check_device(rs_context *ctx) {
         DeviceGuard dg(ctx->device);
         check(hipDeviceSynchronize());
         check(hipGetLastError());
-        uint32_t give_ups = 0;
-        check(hipMemcpy(&give_ups, ctx->d_pair_timeouts, 4, hipMemcpyDeviceToHost));
-        if (give_ups) {
-            g_last_error = "pair encode: " + std::to_string(give_ups) +
-                           " waves gave up waiting for their partner workgroup's half (results invalid)";
-            return RS_ERR_DEVICE;
-        }
         return RS_OK;
     });
 }

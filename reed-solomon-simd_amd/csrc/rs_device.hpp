@@ -191,26 +191,7 @@ struct MonoArgs {
     // so the single-stripe kernel's argument loads stay as they were.
     uint32_t stripes = 1;
     uint64_t src_bstride[2] = {0, 0}, dst_bstride = 0;
-    // Pair encode (launch_mono_pair): a transform of 2^(L+1) rows split over two
-    // workgroups per pack, each holding one half (2^L rows) -- the IFFT's and the
-    // FFT's layers below the top are independent per half; the two top layers
-    // need both halves' values, handed over lane to lane as 8-byte granules
-    // {epoch, word} (write-through agent-scope stores, polled until every tag
-    // is this launch's epoch).  ifft_img / fft_img are then the L-row images of
-    // the lower half (2 t); the upper half adds 1.  Read only by that kernel.
-    // The two top layers (IFFT b' = a ^ b, a' = a ^ b' mI; FFT a'' = a' ^ b' mF,
-    // b'' = b' ^ a'') fold into ONE multiply, a'' = a ^ b' (mI + mF): perm tables
-    // are linear in the multiplier, so `top` is the XOR of the two tables.
-    uint32_t epoch = 0;                 // this launch's tag, never 0
-    uint64_t *xchg = nullptr;           // 16 * packs_per_xcd * threads * 2^(LR+1) granules
-    uint32_t *pair_timeouts = nullptr;  // bounded-spin give-ups (rs_check_device reports them)
-    uint32_t top[20] = {};              // table of mI + mF (4-element format)
 };
-// The pair kernel exists for 2^L-row halves with kMonoPairMinL <= L <= kMonoPairMaxL.
-constexpr int kMonoPairMinL = 8, kMonoPairMaxL = 10;
-// Pair encode of a 2^(L+1)-row transform (modes kMonoEncodeHigh / Low, one
-// chunk, one stripe, 4-element packs); grid 2 * 8 * packs_per_xcd.
-hipError_t launch_mono_pair(int mode, int L, const MonoArgs &A, hipStream_t stream);
 // hipErrorNotSupported: no column kernel for this L (7 <= L <= 12 are built).
 hipError_t launch_mono(int mode, int L, const MonoArgs &A, hipStream_t stream);
 // Variant launch_mono picks: LDS-staged twiddles (single chunk, 2 rows per

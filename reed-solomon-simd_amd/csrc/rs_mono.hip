@@ -1034,70 +1034,6 @@ __device__ __forceinline__ void split_top(Col<L, LR, E> &c, uint32_t *plane, uin
     }
 }
 
-// Pair encode: the two top layers of a 2^(L+1)-row transform whose halves
-// (2^L rows each) sit in workgroups b and b ^ 8.  After the half's IFFT (all
-// its L layers: the layers below the top act within a half) both workgroups
-// have the same placement, so lane t of one needs exactly lane t of the other:
-// each lane publishes its rows as 8-byte granules {epoch, word} with
-// write-through agent-scope stores and polls the partner's granules with
-// agent-scope loads until every tag is this launch's epoch (a granule is one
-// aligned 8-byte store, so a matching tag carries its word; MI355X_MICROARCH
-// "visibility", hand-off R2).  Then, with a = lower-half and b = upper-half
-// value of the lane's row position (engine_naive.rs:64-68, 96-100):
-//   IFFT top layer  b' = a ^ b,  a' = a ^ b' mI;   FFT top layer  a'' = a' ^ b' mF,  b'' = b' ^ a''
-// so a'' = a ^ b' (mI + mF): ONE multiply by the XOR of the two tables
-// (A.top; perm tables are linear in the multiplier).  The lower half keeps
-// a'', the upper b''.  The spin is bounded: a workgroup whose partner never
-// publishes (cannot happen while both are resident: 2 * packs workgroups of
-// one launch) counts a give-up in A.pair_timeouts (rs_check_device fails)
-// instead of hanging the device.
-#ifndef RS_MONO_PAIR_SPIN
-#define RS_MONO_PAIR_SPIN (1u << 18)
-#endif
-typedef __attribute__((address_space(1))) uint64_t g_u64;
-template <int L, int LR>
-__device__ __forceinline__ void pair_top(Col<L, LR, 4> &c, const MonoArgs &A, uint32_t slot, uint32_t half) {
-    constexpr int R = 1 << LR;
-    constexpr uint32_t T = 1u << (L - LR);  // threads
-    constexpr int NG = 2 * R;                // granules per thread: (low, high) word of each row
-    g_u64 *x = (g_u64 *)(A.xchg);
-    g_u64 *mine = x + (uint64_t(slot) * 2 + half) * (NG * T) + threadIdx.x;
-    g_u64 *theirs = x + (uint64_t(slot) * 2 + (half ^ 1u)) * (NG * T) + threadIdx.x;
-    const uint64_t tag = uint64_t(A.epoch) << 32;
-    static_for<0, R>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        __hip_atomic_store(mine + (2 * i) * T, tag | c.lo[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(mine + (2 * i + 1) * T, tag | c.hi[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    });
-    asm volatile("" ::: "memory");  // publish before polling
-    uint32_t p[NG];
-    for (uint32_t spin = 0;; ++spin) {
-        bool ok = true;
-        static_for<0, NG>([&](auto kc) {
-            constexpr int k = decltype(kc)::value;
-            const uint64_t v = __hip_atomic_load(theirs + k * T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            p[k] = uint32_t(v);
-            ok = ok && uint32_t(v >> 32) == A.epoch;
-        });
-        if (__all(ok)) break;
-        if (spin >= RS_MONO_PAIR_SPIN) {
-            if ((threadIdx.x & 63u) == 0) atomicAdd(A.pair_timeouts, 1u);
-            break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    static_for<0, R>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        uint32_t al = half ? p[2 * i] : c.lo[i], ah = half ? p[2 * i + 1] : c.hi[i];
-        uint32_t bl = half ? c.lo[i] : p[2 * i], bh = half ? c.hi[i] : p[2 * i + 1];
-        bl ^= al;  // b'
-        bh ^= ah;
-        gf_muladd4(al, ah, bl, bh, A.top);  // a''
-        c.lo[i] = half ? bl ^ al : al;      // b'' = b' ^ a''
-        c.hi[i] = half ? bh ^ ah : ah;
-    });
-}
-
 // ---------------------------------------------------------------------------
 // eval_poly fused into the staged decode (rs_eval.hip has the standalone
 // kernel; same reduction to 2^L points, src/engine/utils.rs:20-31).  Thread t
@@ -1257,13 +1193,11 @@ __device__ __forceinline__ uint32_t priv_layer(uint32_t t) {
 #define RS_MONO_LDS_PF 2
 #endif
 
-template <int L, int LR, int MODE, bool STAGED, bool BATCH, bool SPLIT, int E, bool PAIR>
+template <int L, int LR, int MODE, bool STAGED, bool BATCH, bool SPLIT, int E>
 __device__ __forceinline__ void mono_body(const MonoArgs &A) {
     using C = Col<L, LR, E>;
     using G = Stage<L, LR, SPLIT, E>;
     static_assert(!SPLIT || (STAGED && MODE == kMonoDecode), "split plan: staged decode only");
-    static_assert(!PAIR || (STAGED && MODE != kMonoDecode && !BATCH && !SPLIT && E == 4 && G::WB > 0),
-                  "pair kernel: staged single-stripe encode with wave bits");
     static_assert(STAGED || E == 4, "2-element packs: staged kernel only");
     constexpr int R = 1 << LR;
     constexpr uint32_t T = 1u << (L - LR);
@@ -1276,20 +1210,15 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
     if (threadIdx.x == 0 && blockIdx.x < 4096) g_mono_stamps[blockIdx.x][12] = __builtin_amdgcn_s_memrealtime();
 #endif
     const uint32_t b = blockIdx.x;
-    // pair kernel: workgroups b and b ^ 8 (one XCD) hold the lower / upper half
-    // of pack (b % 8) * packs_per_xcd + b / 16 (pair slot = b without bit 3)
-    const uint32_t half = PAIR ? (b >> 3) & 1u : 0u;
-    const uint32_t pk = (b & 7u) * A.packs_per_xcd + (PAIR ? b >> 4 : b >> 3);
-    if (pk >= A.packs) return;  // (both workgroups of a pair)
+    const uint32_t pk = (b & 7u) * A.packs_per_xcd + (b >> 3);
+    if (pk >= A.packs) return;
     const StripeBases sb = BATCH ? stripe_bases(A, blockIdx.y) : StripeBases{A.src[0].base, A.src[1].base,
                                                                              const_cast<uint8_t *>(A.dst.base)};
     // the pack's bytes in the caller's rows (tails: shards.rs:38-74)
     const PackIO io = E == 4 ? pack_io(A.fmt, pk) : pack_io2(A.fmt, pk);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // (pair: the upper half of a 2^(L+1)-row transform on skew offset 2t * 2^L is
-    // the 2^L-row transform on offset (2t + 1) * 2^L, layers below the top)
-    const uint32_t ii = A.ifft_img + half, fi = A.fft_img + half;
+    const uint32_t ii = A.ifft_img, fi = A.fft_img;
     const uint32_t *img_i = A.img + uint64_t(ii) * A.img_words;
     const uint32_t *img_f = A.img + uint64_t(fi) * A.img_words;
     const uint32_t *img_d = A.img + uint64_t(ii ^ fi) * A.img_words;
@@ -1343,7 +1272,7 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
             lw[1] = A.lw_fold[i0 + 1];
         }
         uint32_t w[2 << LR];
-        issue_col<L, LR, SPLIT, E>(A, half, io, sb, w, lane, wave, live);  // (pair: rows half * 2^L ..)
+        issue_col<L, LR, SPLIT, E>(A, 0, io, sb, w, lane, wave, live);
         // phase-1 tables (a wave that skips phase 1 reads one table: no branch
         // around the loads); B0: layer 0's go into the region first, the
         // layers above when layer 0 has read them (run_seq's hook)
@@ -1485,7 +1414,6 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
         } else if constexpr (G::WB > 0) {
             run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 1 : -1>(ts, c, plane, lane, wave, issue3, true, live,
                                                                    write1);
-            if constexpr (PAIR) pair_top<L, LR>(c, A, ((b >> 4) << 3) | (b & 7u), half);
             RS_MSTAMP(5);
             using SF = SeqOf<L, LR, true>;
             constexpr int NLF = num_layers(SF::v);
@@ -1504,7 +1432,7 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
             run_seq<L, LR, true, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, NoHook{});
         }
         RS_MSTAMP(10);
-        store_col<L, LR, DEC, SPLIT>(A, ri, half, io, sb, c, lane, wave);
+        store_col<L, LR, DEC, SPLIT>(A, ri, 0, io, sb, c, lane, wave);
         RS_MSTAMP(11);
     } else if constexpr (MODE == kMonoEncodeHigh) {
         // rate_high.rs:44-87: recovery = FFT_0(XOR_c IFFT_{c n + n}(chunk c))
@@ -1544,14 +1472,8 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
 
 template <int L, int LR, int MODE, bool STAGED, bool BATCH, bool SPLIT, int E>
 __global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
-    mono_body<L, LR, MODE, STAGED, BATCH, SPLIT, E, false>(A);
+    mono_body<L, LR, MODE, STAGED, BATCH, SPLIT, E>(A);
 }
-// pair encode (MonoArgs "Pair encode"): 2 workgroups per pack, 2^L rows each
-template <int L, int LR, int MODE>
-__global__ void __launch_bounds__(1 << (L - LR)) k_mono_pair(const MonoArgs A) {
-    mono_body<L, LR, MODE, true, false, false, 4, true>(A);
-}
-
 #ifndef RS_MONO_LR10
 #define RS_MONO_LR10 1
 #endif
@@ -1632,45 +1554,7 @@ hipError_t launch_m(int L, const MonoArgs &A, hipStream_t s) {
     }
 }
 
-template <int L, int MODE>
-hipError_t launch_pair_l(const MonoArgs &A, hipStream_t s) {
-    constexpr int LR = 1;
-    const size_t lds = size_t(Stage<L, LR, false, 4>::words_enc) * 4;
-    static bool attr_set = false;  // benign race: idempotent attribute call
-    if (!attr_set && lds > 65536) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mono_pair<L, LR, MODE>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
-    k_mono_pair<L, LR, MODE><<<16u * A.packs_per_xcd, 1 << (L - LR), lds, s>>>(A);
-    snprintf(launch_name_buf(), kLaunchNameBytes, "k_mono_pair<%d, %d, %d>", L, LR, MODE);
-    return hipGetLastError();
-}
-
-template <int MODE>
-hipError_t launch_pair_m(int L, const MonoArgs &A, hipStream_t s) {
-    switch (L) {
-        case 8: return launch_pair_l<8, MODE>(A, s);
-        case 9: return launch_pair_l<9, MODE>(A, s);
-        case 10: return launch_pair_l<10, MODE>(A, s);
-        default: return hipErrorNotSupported;
-    }
-}
-
 }  // namespace
-
-hipError_t launch_mono_pair(int mode, int L, const MonoArgs &A, hipStream_t s) {
-    static_assert(kMonoPairMinL == 8 && kMonoPairMaxL == 10, "pair kernel instantiations");
-    if (A.packs == 0) return hipSuccess;
-    if (A.elems != 4 || A.stripes != 1 || A.chunks != 1 || !A.xchg || !A.epoch || !A.pair_timeouts)
-        return hipErrorInvalidValue;
-    switch (mode) {
-        case kMonoEncodeHigh: return launch_pair_m<kMonoEncodeHigh>(L, A, s);
-        case kMonoEncodeLow: return launch_pair_m<kMonoEncodeLow>(L, A, s);
-        default: return hipErrorNotSupported;
-    }
-}
 
 bool mono_staged(int L, uint32_t chunks) { return L >= 7 && staged_l(L) && chunks == 1; }
 bool mono_split(int L) { return split_l(L) && staged_l(L); }

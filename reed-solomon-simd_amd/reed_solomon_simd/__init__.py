@@ -23,8 +23,7 @@ import os
 from typing import Dict, Iterable, List, Optional, Tuple
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# RS_MI355X_LIB: an alternative build of the same library (A/B timing of kernel variants)
-LIB_PATH = os.environ.get("RS_MI355X_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "librs_mi355x.so")
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librs_mi355x.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -139,18 +138,27 @@ _sig("rs_check_device", _int, _vp)
 
 
 _sig("rs_mono_enable", _int, _vp, _int)
+_sig("rs_release_stream_scratch", _int, _vp, _vp)
+
+
+def release_stream_scratch(stream=None, ctx=None) -> None:
+    """Synchronize `stream` and free the context's device scratch for it (rs_release_stream_scratch)."""
+    ctx = ctx or default_context()
+    st = _lib.rs_release_stream_scratch(ctx.handle, _stream(stream))
+    if st != 0:
+        raise DeviceError(_lib.rs_last_device_error().decode())
 
 
 def mono_enable(enable=True, ctx=None) -> None:
     """Column kernel (one workgroup per pack): False = never, True = where fastest (default),
     2 = also multi-chunk and 2^11 / 2^12-row transforms; + 4 no split decode plan, + 8 4-element
-    packs only, + 16 2-element packs everywhere, + 32 pair encode (rs_mono_enable)."""
+    packs only, + 16 2-element packs everywhere (rs_mono_enable)."""
     ctx = ctx or default_context()
     _lib.rs_mono_enable(ctx.handle, int(enable))
 
 
 def check_device(ctx=None) -> None:
-    """Synchronize; raise DeviceError if an in-kernel barrier wait timed out."""
+    """Synchronize the context's device; raise DeviceError if an earlier asynchronous launch failed."""
     ctx = ctx or default_context()
     st = _lib.rs_check_device(ctx.handle)
     if st != 0:
@@ -958,10 +966,18 @@ class ShardedEncoder:
         if self._encode_slice is not None:
             self._encode_slice(cols, out)
             return
+        if self.stream is None:
+            encode_device(self.N, self.M, cols.shape[1], cols, out, rate_=self.rate, ctx=self.ctx)
+            return
+        import torch
+        cur = torch.cuda.current_stream()
+        # a caller-supplied stream: the encode waits for what the current stream has
+        # queued -- the writes of `cols`, and (through the previous call's work.wait())
+        # the all-gathers still reading `out` = pieces[c] -- and the collectives, which
+        # follow the current stream, wait for the encode
+        self.stream.wait_stream(cur)
         encode_device(self.N, self.M, cols.shape[1], cols, out, stream=self.stream, rate_=self.rate, ctx=self.ctx)
-        if self.stream is not None:
-            import torch
-            torch.cuda.current_stream().wait_stream(self.stream)  # collectives follow the current stream
+        cur.wait_stream(self.stream)
 
     def encode_local(self, orig_cols) -> None:
         """Encode this rank's [N x w] columns into self.part (one device call)."""

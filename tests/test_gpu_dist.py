@@ -22,7 +22,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, N, M, S, chunks, q):
+def _worker(rank, world, port, N, M, S, chunks, side, q):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "reed-solomon-simd_amd"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -36,13 +36,20 @@ def _worker(rank, world, port, N, M, S, chunks, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
-        orig = O.generate_original(N, S, 77)
-        enc = rs.ShardedEncoder(N, M, S, device="cuda:0", chunks=chunks)
-        cols = torch.from_numpy(orig[:, rank * enc.w:(rank + 1) * enc.w].copy()).cuda()
+        # side: the encoder runs on a caller-supplied stream that is not the current
+        # one; the inputs of every round are written on the current stream just before
+        # the call, and the pieces are reused round after round
+        stream = torch.cuda.Stream() if side else None
+        enc = rs.ShardedEncoder(N, M, S, device="cuda:0", chunks=chunks, stream=stream)
+        origs = [O.generate_original(N, S, 77 + it) for it in range(3)]
+        d_cols = [torch.from_numpy(o[:, rank * enc.w:(rank + 1) * enc.w].copy()).cuda() for o in origs]
+        cols = torch.empty_like(d_cols[0])
         d_rec = torch.zeros((M, S), dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()
         ok = True
-        for _ in range(2):
+        for it, orig in enumerate(origs):
             d_rec.zero_()
+            cols.copy_(d_cols[it])  # on the current stream
             enc(cols, d_rec)
             torch.cuda.synchronize()
             got = d_rec.cpu().numpy()
@@ -59,14 +66,15 @@ def _worker(rank, world, port, N, M, S, chunks, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("N,M,S,chunks", [(1024, 1024, 8192, 4), (700, 300, 2048, 2)])
-def test_sharded_pipelined_encode_two_ranks_one_gpu(N, M, S, chunks):
+@pytest.mark.parametrize("N,M,S,chunks,side", [(1024, 1024, 8192, 4, False), (700, 300, 2048, 2, False),
+                                               (1024, 1024, 8192, 4, True)])
+def test_sharded_pipelined_encode_two_ranks_one_gpu(N, M, S, chunks, side):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, N, M, S, chunks, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, N, M, S, chunks, side, q)) for r in range(2)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=110) for _ in procs)

@@ -420,62 +420,67 @@ def test_engine_host_slices_match_oracle(torch, rs, which):
 
 
 # ---------------------------------------------------------------------------
-# pair encode (rs_mono.hip pair_top): one-chunk encodes of 2^9 .. 2^11 rows over
-# at most 128 packs run as two workgroups per pack with an in-launch hand-off
+# per-stream device scratch (rs_mi355x.h "Thread-safety"): capped per context
 
-PAIR_CASES = [
-    # (rate, N, M, S): 2^9, 2^10, 2^11 transform rows; tails; 1 .. 128 packs
-    ("high", 300, 300, 64), ("high", 512, 512, 1024), ("default", 1024, 1024, 1024),
-    ("high", 700, 1000, 256), ("high", 1000, 1000, 8), ("high", 2048, 2048, 64),
-    ("high", 1500, 2000, 1000), ("low", 1000, 1000, 512), ("low", 400, 300, 136),
-    ("low", 2000, 1200, 64), ("high", 1024, 1024, 2),
-]
-
-
-@pytest.mark.parametrize("rate,N,M,S", PAIR_CASES)
-def test_pair_encode_matches_oracle(torch, rs, rate, N, M, S):
-    """The pair kernel (rs_mono_enable + 32) bit-exact against the oracle, and the default
-    (one workgroup per pack) likewise."""
-    orig = O.generate_original(N, S, (N + 7 * M + S) & 0xFF)
-    want = O.encode(rate, orig, M)
-    rs.mono_enable(1 | 32)
-    try:
-        got = gpu_encode(torch, rs, rate, orig, M)
-        rs.check_device()  # also fails if a pair workgroup gave up waiting for its partner
-    finally:
-        rs.mono_enable(1)
-    assert np.array_equal(got, want)
-    assert np.array_equal(gpu_encode(torch, rs, rate, orig, M), want)
-
-
-def test_pair_encode_under_uneven_load(torch, rs):
-    """Pair hand-offs while another stream keeps the CUs busy with a large multi-pass
-    encode (partners dispatched at different times, consumers L1-warm from the previous
-    round's reads of the same granule lines): 60 back-to-back pair encodes of
-    alternating inputs on one stream, every result checked."""
-    N, M, S = 1024, 1024, 1024
-    origs = [O.generate_original(N, S, k) for k in (11, 12)]
+def test_stream_scratch_is_capped_and_released(torch, rs):
+    """Pass-kernel encodes (which need work buffers) on more streams than the context
+    keeps scratch for (RS_MAX_STREAM_WORKSPACES = 16): every result equals the oracle,
+    the least recently used stream's scratch is evicted behind a device synchronize, and
+    release_stream_scratch frees one stream's scratch on demand."""
+    N, M, S = 4096, 4096, 256
+    origs = [O.generate_original(N, S, 90 + k) for k in range(2)]
     wants = [O.encode("high", o, M) for o in origs]
     d_o = [_dev(torch, o) for o in origs]
-    outs = [torch.empty((M, S), dtype=torch.uint8, device="cuda") for _ in range(60)]
-    big_n, big_s = 16384, 4096
-    b_o = torch.randint(0, 256, (big_n, big_s), dtype=torch.uint8, device="cuda")
-    b_r = torch.empty((big_n, big_s), dtype=torch.uint8, device="cuda")
-    s_big, s_pair = torch.cuda.Stream(), torch.cuda.Stream()
+    streams = [torch.cuda.Stream() for _ in range(20)]
+    outs = [torch.empty((M, S), dtype=torch.uint8, device="cuda") for _ in streams]
     torch.cuda.synchronize()
-    rs.mono_enable(1 | 32)
-    try:
-        for rep in range(3):
-            rs.encode_device(big_n, big_n, big_s, b_o, b_r, stream=s_big)
-            for k in range(20):
-                j = rep * 20 + k
-                rs.encode_device(N, M, S, d_o[j & 1], outs[j], stream=s_pair)
+    for rep in range(2):
+        for k, st in enumerate(streams):
+            st.wait_stream(torch.cuda.current_stream())
+            rs.encode_device(N, M, S, d_o[(k + rep) & 1], outs[k], rate_=rs.RATE_HIGH, stream=st)
         torch.cuda.synchronize()
-        rs.check_device()
+        for k, o in enumerate(outs):
+            assert np.array_equal(o.cpu().numpy(), wants[(k + rep) & 1]), (rep, k)
+    for st in streams:
+        rs.release_stream_scratch(st)
+    rs.release_stream_scratch(streams[0])  # already released: no-op
+    rs.check_device()
+
+
+def test_work_moves_between_contexts(torch, rs):
+    """EncoderWork / DecoderWork handed to a second context: the work records
+    its context's device; on the same device its buffers are reused, and the results of
+    both contexts equal the oracle."""
+    ctx2 = rs.Context(0)
+    try:
+        orig = O.generate_original(300, 1024, 5)
+        want = O.encode("high", orig, 200)
+        enc = rs.rate.HighRateEncoder(300, 200, 1024)
+        for row in orig:
+            enc.add_original_shard(row.tobytes())
+        assert b"".join(enc.encode().recovery_iter()) == want.tobytes()
+        _, work = enc.into_parts()
+        enc2 = rs.rate.HighRateEncoder(300, 200, 1024, ctx=ctx2, work=work)
+        for row in orig:
+            enc2.add_original_shard(row.tobytes())
+        assert b"".join(enc2.encode().recovery_iter()) == want.tobytes()
+        dec = rs.rate.HighRateDecoder(300, 200, 1024, ctx=ctx2)
+        for i in range(100, 300):
+            dec.add_original_shard(i, orig[i].tobytes())
+        for i in range(100):
+            dec.add_recovery_shard(i, want[i].tobytes())
+        assert all(v == orig[i].tobytes() for i, v in dec.decode().restored_original_iter())
+        _, dwork = dec.into_parts()
+        dec2 = rs.rate.HighRateDecoder(300, 200, 1024, work=dwork)
+        for i in range(100, 300):
+            dec2.add_original_shard(i, orig[i].tobytes())
+        for i in range(100):
+            dec2.add_recovery_shard(i, want[i].tobytes())
+        got = dict(dec2.decode().restored_original_iter())
+        assert sorted(got) == list(range(100)) and all(got[i] == orig[i].tobytes() for i in got)
+        del enc2, dec2
     finally:
-        rs.mono_enable(1)
-    for j, o in enumerate(outs):
-        assert np.array_equal(o.cpu().numpy(), wants[j & 1]), f"encode {j}"
+        ctx2.close()
 
 
 def test_two_streams_share_one_context(torch, rs):

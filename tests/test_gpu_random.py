@@ -1,0 +1,238 @@
+"""Seeded randomised GPU parity (VERDICT r02 "missing" item 1).
+
+The idea of the reference's fuzzers -- random original / recovery counts, random loss
+sets, every rate, reused working space (/root/reference/examples/test-random-roundtrips.rs:72-178)
+and random counts with small shards (/root/reference/tests/integration_test.rs:237-295) --
+run against the CPU oracle through the device API and the object API.
+
+The draws come from one fixed seed, so a failure names a reproducible case.  They are
+biased to straddle every routing threshold of rs_codec.cpp / rs_mono.hip:
+  * column-kernel transform sizes 2^6 / 2^7 and 2^11 / 2^12 rows (encode n = pow2(M)
+    high, pow2(N) low; decode work rows pow2(pow2(M) + N) high, pow2(pow2(N) + M) low);
+  * 4-element pack counts 192 / 193 (2-element decode packs, e2_max_packs) and
+    256 / 257 (mono_max_packs), i.e. shard sizes around 1536 and 2048 bytes;
+  * one chunk versus several (HighRate N > pow2(M), LowRate M > pow2(N));
+  * split versus unsplit decode plans (restored rows in one half of the work rows or
+    in both), contiguous and scattered losses, all losses recoverable;
+  * shard sizes that are not multiples of 64 (tail blocks).
+Each case is compared with the oracle once.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED_2026
+RATE = {"default": 0, "high": 1, "low": 2}
+P2 = lambda x: 1 << max(0, int(x - 1).bit_length())  # noqa: E731  next power of two
+
+
+def _high(N, M, rate):
+    if rate == "high":
+        return True
+    if rate == "low":
+        return False
+    pn, pm = P2(N), P2(M)
+    return pn > pm if pn != pm else N <= M
+
+
+def _supported(N, M, rate):
+    if not (0 < N < 65536 and 0 < M < 65536):
+        return False
+    if rate == "default":
+        return min(P2(N), P2(M)) + max(N, M) <= 65536
+    return (P2(M) + N if rate == "high" else P2(N) + M) <= 65536
+
+
+def _even(rng, lo, hi):
+    return int(rng.integers(lo // 2, hi // 2 + 1)) * 2
+
+
+def _draw(rng):
+    """One (rate, N, M, S, kind) draw, biased to a routing threshold."""
+    kind = ["enc_L", "packs", "chunks", "low_chunks", "tail", "dec_L", "split", "small"][int(rng.integers(0, 8))]
+    rate = ["default", "high", "low"][int(rng.integers(0, 3))]
+    S = _even(rng, 2, 512)
+    if kind == "enc_L":  # transform size straddles 2^6/2^7 or 2^11/2^12 rows
+        L = int(rng.choice([6, 7, 11, 12]))
+        big = int(rng.integers((1 << (L - 1)) + 1, (1 << L) + 1))
+        small = int(rng.integers(1, big + 1))
+        rate = rng.choice(["high", "low"])
+        N, M = (small, big) if rate == "high" else (big, small)
+        S = _even(rng, 2, 256 if L >= 11 else 1024)
+    elif kind == "packs":  # 192 / 193 and 256 / 257 4-element packs
+        S = int(rng.choice([1536, 1528, 1544, 1540, 2048, 2040, 2056, 2050, 1024 + 512 + 8]))
+        N = int(rng.integers(100, 1100))
+        M = int(rng.integers(100, 1100))
+    elif kind == "chunks":  # HighRate, several chunks of pow2(M) rows
+        M = int(rng.integers(1, 600))
+        N = int(rng.integers(P2(M) + 1, 4 * P2(M) + 2))
+        rate = "high"
+        S = _even(rng, 2, 256)
+    elif kind == "low_chunks":  # LowRate, several output chunks
+        N = int(rng.integers(1, 600))
+        M = int(rng.integers(P2(N) + 1, 4 * P2(N) + 2))
+        rate = "low"
+        S = _even(rng, 2, 256)
+    elif kind == "tail":  # shard sizes that are not multiples of 64
+        N = int(rng.integers(1, 1500))
+        M = int(rng.integers(1, 1500))
+        S = _even(rng, 2, 700)
+        if S % 64 == 0:
+            S += 2
+    elif kind == "dec_L":  # decode work rows straddle 2^11 / 2^12
+        M = int(rng.integers(1, 1100))
+        target = int(rng.integers(1900, 2200))
+        N = max(1, target - P2(M))
+        rate = "high"
+        S = _even(rng, 2, 512)
+    elif kind == "split":  # headline-like shapes: restored rows in one half or in both
+        M = int(rng.choice([256, 512, 1000, 1024]))
+        N = int(rng.integers(M // 2, 2 * M))
+        rate = "high"
+        S = _even(rng, 64, 1024)
+    else:
+        N = int(rng.integers(1, 300))
+        M = int(rng.integers(1, 300))
+    # keep the oracle's share of the run small: at most ~6 MB of shards per case
+    while (N + M) * S > 6 << 20 and S > 2:
+        S = max(2, (S // 4) * 2)
+    return str(rate), int(N), int(M), int(S), kind
+
+
+def _losses(rng, N, M, rate):
+    """(original_present, recovery_present): contiguous, scattered, head/tail, one, all."""
+    lmax = min(N, M)
+    how = ["random", "run", "tail", "head", "one", "max"][int(rng.integers(0, 6))]
+    if how == "one":
+        L = 1
+    elif how == "max":
+        L = lmax
+    else:
+        L = int(rng.integers(1, lmax + 1)) if rng.random() < 0.5 else max(1, int(lmax * rng.random() * 0.05))
+    op = np.ones(N, np.uint8)
+    if how in ("random", "max"):
+        op[rng.choice(N, L, replace=False)] = 0
+    elif how == "run":
+        a = int(rng.integers(0, N - L + 1))
+        op[a:a + L] = 0
+    elif how == "tail":
+        op[N - L:] = 0
+    elif how == "head":
+        op[:L] = 0
+    else:
+        op[int(rng.integers(0, N))] = 0
+    L = int((op == 0).sum())
+    extra = int(rng.integers(0, 3))
+    rp = np.zeros(M, np.uint8)
+    rp[rng.choice(M, min(M, L + extra), replace=False)] = 1
+    return op, rp, how
+
+
+def _cases(count):
+    rng = np.random.default_rng(SEED)
+    out = []
+    while len(out) < count:
+        rate, N, M, S, kind = _draw(rng)
+        if not _supported(N, M, rate):
+            continue
+        op, rp, how = _losses(rng, N, M, rate)
+        seed = int(rng.integers(0, 256))
+        out.append(pytest.param(rate, N, M, S, op, rp, seed, id=f"{len(out)}-{kind}-{rate}-{N}x{M}x{S}-{how}"))
+    return out
+
+
+CASES = _cases(320)
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.skip("no GPU")
+    return t
+
+
+@pytest.fixture(scope="module")
+def rs(torch):
+    import reed_solomon_simd
+    return reed_solomon_simd
+
+
+def _dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.parametrize("rate,N,M,S,op,rp,seed", CASES)
+def test_random_encode_decode_device(torch, rs, rate, N, M, S, op, rp, seed):
+    orig = O.generate_original(N, S, seed)
+    want = O.encode(rate, orig, M)
+    d_orig = _dev(torch, orig)
+    d_rec = torch.full((M, S), 0xEE, dtype=torch.uint8, device="cuda")
+    rs.encode_device(N, M, S, d_orig, d_rec, rate_=RATE[rate])
+    torch.cuda.synchronize()
+    assert np.array_equal(d_rec.cpu().numpy(), want), "encode"
+    # decode: missing rows of the inputs hold junk the decoder must never read
+    d_o = _dev(torch, np.where(op[:, None] == 1, orig, 0xA5).astype(np.uint8))
+    d_r = _dev(torch, np.where(rp[:, None] == 1, want, 0x5A).astype(np.uint8))
+    d_out = torch.full((N, S), 0x33, dtype=torch.uint8, device="cuda")
+    rs.decode_device(N, M, S, d_o, op, d_r, rp, d_out, rate_=RATE[rate])
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy()
+    miss = op == 0
+    assert np.array_equal(got[miss], orig[miss]), "restored originals"
+    assert np.all(got[~miss] == 0x33), "present rows of the output must not be written"
+
+
+def _chains(count, steps):
+    rng = np.random.default_rng(SEED + 1)
+    out = []
+    for c in range(count):
+        seq = []
+        while len(seq) < steps:
+            rate = ["default", "high", "low"][int(rng.integers(0, 3))]
+            N, M = int(rng.integers(1, 1200)), int(rng.integers(1, 1200))
+            S = _even(rng, 2, 320)
+            if not _supported(N, M, rate):
+                continue
+            op, rp, _ = _losses(rng, N, M, rate)
+            seq.append((rate, N, M, S, op, rp, int(rng.integers(0, 256)), bool(rng.integers(0, 2))))
+        out.append(pytest.param(seq, id=f"chain{c}"))
+    return out
+
+
+@pytest.mark.parametrize("seq", _chains(24, 5))
+def test_random_work_reuse(rs, seq):
+    """One encoder and one decoder live through a sequence of shapes and rates: each step
+    either resets the object (DefaultRate reset, rate switches included, rate_default.rs:161-206)
+    or hands its working space to a new object of the step's rate (into_parts -> new(.., work),
+    src/rate.rs:129-139, 206-218); every result equals the oracle."""
+    cls_e = {"default": rs.ReedSolomonEncoder, "high": rs.rate.HighRateEncoder, "low": rs.rate.LowRateEncoder}
+    cls_d = {"default": rs.ReedSolomonDecoder, "high": rs.rate.HighRateDecoder, "low": rs.rate.LowRateDecoder}
+    enc = dec = None
+    for rate, N, M, S, op, rp, seed, handoff in seq:
+        orig = O.generate_original(N, S, seed)
+        want = O.encode(rate, orig, M)
+        if enc is None or handoff or type(enc) is not cls_e[rate]:
+            work = enc.into_parts()[1] if enc is not None else None
+            enc = cls_e[rate](N, M, S, work=work)
+        else:
+            enc.reset(N, M, S)
+        for row in orig:
+            enc.add_original_shard(row.tobytes())
+        rec = b"".join(enc.encode().recovery_iter())
+        assert rec == want.tobytes(), "encode"
+        if dec is None or handoff or type(dec) is not cls_d[rate]:
+            work = dec.into_parts()[1] if dec is not None else None
+            dec = cls_d[rate](N, M, S, work=work)
+        else:
+            dec.reset(N, M, S)
+        for i in np.flatnonzero(op):
+            dec.add_original_shard(int(i), orig[i].tobytes())
+        for i in np.flatnonzero(rp):
+            dec.add_recovery_shard(int(i), want[i].tobytes())
+        got = dict(dec.decode().restored_original_iter())
+        assert sorted(got) == [int(i) for i in np.flatnonzero(op == 0)]
+        assert all(got[i] == orig[i].tobytes() for i in got), "decode"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build reed-solomon-simd_amd/lib/variants/librs_mi355x_<name>.so: the given sources
 # recompiled with extra hipcc flags, linked with the main build's other objects
-# (A/B of kernel variants: RS_MI355X_LIB=<path> selects it at import).
+# (A/B of kernel variants: tools/ab_common.sh puts it in place of the main build).
 #   bash tools/build_variant.sh <name> "<src> [src...]" -DFOO ...
 set -euo pipefail
 NAME=$1; SRCS=$2; shift 2
