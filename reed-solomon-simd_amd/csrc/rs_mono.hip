@@ -143,12 +143,19 @@ constexpr Map seg_map(int L, int LR, int lo, const int *order, int no) {
 // layers of both transforms and the formal derivative's cross-half term run
 // in one exchange (split_top), and only the half holding restored rows runs
 // the rest of the FFT.
-template <int L, int LR, bool SPLIT = false>
+// SP bit 1 (FLOW, decodes): the FFT leaves the top placement after layer IW
+// instead of WB, so its layers IW-1..0 run with the low bits in-wave -- each
+// wave then holds 2^IW consecutive rows, the waves without restored rows stop
+// there, and those layers reuse the IFFT's phase-1 tables
+template <int L, int LR, int SP = 0>
 struct Plan {
+    static constexpr bool SPLIT = (SP & 1) != 0, FLOW = (SP & 2) != 0;
     static constexpr int IW = LR + 6, WB = L - IW - (SPLIT ? 1 : 0), R = 1 << LR;
     static_assert(WB >= 0 && L - IW <= 4, "column kernel: 6 lane bits + LR register bits + up to 4 wave bits");
     static_assert(!SPLIT || WB >= 1, "split plan: at least one wave bit below the top bit");
     static constexpr int TOP = SPLIT ? L - 1 : L;  // layers [0, TOP) run in the sequences
+    // lowest FFT layer of the top placement (the FFT's low segment: layers FLO-1..0)
+    static constexpr int FLO = FLOW && WB > 0 ? IW : WB;
 
     static constexpr Seq make_ifft() {
         Seq s{};
@@ -185,22 +192,22 @@ struct Plan {
         int bits[16] = {}, order[16] = {}, no = 0;
         Map m = ifft.maps[ifft.count];
         s.maps[0] = m;
-        const int stop = WB;  // FFT layers TOP-1..stop in the IFFT's final placement
+        const int stop = FLO;  // FFT layers TOP-1..stop in the IFFT's final placement
         for (int x = TOP - 1; x >= stop; --x) bits[TOP - 1 - x] = x;
         layers(s, m, LR, bits, TOP - stop);
         if (WB == 0) return s;
-        // segment C: the low IW bits in-wave again, FFT layers WB-1..0
-        for (int x = WB - 1; x >= 0; --x) order[no++] = x;
+        // segment C: the low IW bits in-wave again, FFT layers FLO-1..0
+        for (int x = FLO - 1; x >= 0; --x) order[no++] = x;
         m = seg_map(L, LR, 0, order, no);
         push(s, Op{kOpRemap, -1, 0, 0}, m);
-        for (int x = WB - 1; x >= 0; --x) bits[WB - 1 - x] = x;
-        layers(s, m, LR, bits, WB);
+        for (int x = FLO - 1; x >= 0; --x) bits[FLO - 1 - x] = x;
+        layers(s, m, LR, bits, FLO);
         return s;
     }
     static constexpr Seq fft = make_fft();
 };
 
-template <int L, int LR, bool FFT, bool SPLIT = false>
+template <int L, int LR, bool FFT, int SPLIT = 0>
 struct SeqOf {
     static constexpr const Seq &v = FFT ? Plan<L, LR, SPLIT>::fft : Plan<L, LR, SPLIT>::ifft;
 };
@@ -338,8 +345,10 @@ struct GlobalTabs {
     }
 };
 
-template <int L, int LR, bool SPLIT = false, int E = 4>
+template <int L, int LR, int SP = 0, int E = 4>
 struct Stage {
+    static constexpr bool SPLIT = Plan<L, LR, SP>::SPLIT;
+    static constexpr int FLO = Plan<L, LR, SP>::FLO;
     static constexpr int TW = Fmt<E>::kTW;
     static constexpr uint32_t PC = Fmt<E>::kPC;
     // LDS slot of a table: 20 words in both formats.  A 2-element table is 16
@@ -381,14 +390,14 @@ struct Stage {
     static __device__ __forceinline__ uint32_t atS(uint32_t q) {
         return at(q, [](uint32_t t) {
             if (t < kShI) return sq(t, uint32_t(L - IW));
-            if (t < kShI + kShF) return kShI + sq(t - kShI, uint32_t(L - WB));
+            if (t < kShI + kShF) return kShI + sq(t - kShI, uint32_t(L - FLO));
             return t;  // D tables: one per layer
         });
     }
     static constexpr int IW = LR + 6, WB = L - IW - (SPLIT ? 1 : 0);
     static constexpr uint32_t n = 1u << L, W = 1u << IW;
     // layers of the last (FFT) in-wave phase
-    static constexpr int NB3 = WB > 0 ? WB : L;
+    static constexpr int NB3 = WB > 0 ? FLO : L;
     // B0 = 1: layer 0 of phases 1 and 3 (one table per butterfly) takes turns
     // with the other layers in the private regions, so they fit LDS at L = 11
 #ifndef RS_MONO_B0_MIN_L
@@ -402,7 +411,7 @@ struct Stage {
     static constexpr uint32_t kP3 = (W >> B0) - (W >> NB3);          // tables of phase 3 (layer 0 apart)
     static constexpr uint32_t kL0 = W >> 1;                          // layer-0 tables of a wave region
     static constexpr uint32_t kShI = WB > 0 ? (n >> IW) - 1 : 0;     // shared: IFFT layers IW..L-1
-    static constexpr uint32_t kShF = WB > 0 ? (n >> WB) - 1 : 0;     // shared: FFT layers WB..L-1
+    static constexpr uint32_t kShF = WB > 0 ? (n >> FLO) - 1 : 0;    // shared: FFT layers FLO..L-1
     static constexpr uint32_t kShared = kShI + kShF;
     static constexpr uint32_t kWaves = 1u << (L - LR - 6);
     static constexpr uint32_t plane_words = (E == 4 ? 2 : 1) * n;
@@ -424,7 +433,7 @@ struct Stage {
 // wave-private region: a wave's rows there are 2^IW consecutive rows, so its
 // groups are its own.  Phase 2 (top bits in-wave, wave bits low) reads the
 // region shared by all waves.
-template <int L, int LR, bool SPLIT = false, int E = 4>
+template <int L, int LR, int SPLIT = 0, int E = 4>
 struct LdsTabs {
     using G = Stage<L, LR, SPLIT, E>;
     const uint32_t *priv, *shared, *img_i, *img_f;
@@ -442,7 +451,7 @@ struct LdsTabs {
             slot = (G::n >> G::IW) - (G::n >> x) + G::sg(row >> (x + 1));
             base = shared;
         } else {
-            slot = G::kShI + (G::n >> G::WB) - (G::n >> x) + G::sg(row >> (x + 1));
+            slot = G::kShI + (G::n >> G::FLO) - (G::n >> x) + G::sg(row >> (x + 1));
             base = shared;
         }
 #ifdef RS_MONO_FAKE_TABS  // tools/mono_probe.hip: tables without LDS traffic
@@ -565,7 +574,7 @@ struct NoHook {
 // wave-private table region there that the layers before it have read).  A
 // wave with `pre` false skips the ops before the remap, with `alive` false
 // the ops after it.
-template <int L, int LR, bool FFT, int B0, int KHOOK = -1, bool SPLIT = false, typename TS, typename PreRemap,
+template <int L, int LR, bool FFT, int B0, int KHOOK = -1, int SPLIT = 0, typename TS, typename PreRemap,
           int E, typename Hook = NoHook>
 __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR, E> &c, uint32_t *plane, uint32_t lane, uint32_t wave,
                                         const PreRemap &pre_remap, bool alive = true, bool pre = true,
@@ -628,7 +637,7 @@ __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR, E> &c, uint32_t
 
 // Decode: does this wave hold, after the FFT's remap, any row of A.dst?
 // (there the wave's rows are one block of 2^IW consecutive rows)
-template <int L, int LR, bool SPLIT = false>
+template <int L, int LR, int SPLIT = 0>
 __device__ __forceinline__ bool wave_stores(const MonoArgs &A, uint32_t wave) {
     using S = SeqOf<L, LR, true, SPLIT>;
     constexpr int I = S::v.count;
@@ -669,22 +678,28 @@ __device__ __forceinline__ uint32_t paired_row(uint32_t lane, uint32_t wave, int
 // paired words; finish_col completes them.  Missing rows inside the caller's
 // matrices are read and discarded by the decode's scaling.
 // (2-element packs: the paired words are the 16-bit low and high halves)
-template <int L, int LR, bool SPLIT = false, int E = 4>
+template <int L, int LR, int SPLIT = 0, int E = 4>
 __device__ __forceinline__ void issue_col(const MonoArgs &A, uint32_t chunk, const PackIO &io, const StripeBases &sb,
                                           uint32_t (&w)[2 << LR], uint32_t lane, uint32_t wave, bool live = true) {
     using S = SeqOf<L, LR, false, SPLIT>;
     const uint32_t base = chunk * (1u << L);
     const uint32_t off = io.lo + ((lane & 1u) ? io.hi_delta : 0u);
+    // a row every lane may read (the first source row): lanes without a row of
+    // their own load it and discard it, so every wave issues exactly one load
+    // per word -- a branch around the loads would make the compiler's vmcnt
+    // waits for OLDER loads (the decode's eval_poly inputs) count the loads in
+    // it as absent and wait for these rows too
+    const uint8_t *any_row = A.src[0].row_end > A.src[0].row_begin ? sb.src0 : sb.src1;
     static_for<0, (2 << LR)>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         const uint32_t r = paired_row<S, 0, LR>(lane, wave, j) + base;
         const uint8_t *p = row_ptr(A, sb, r);
-        uint32_t v = 0;
+        const bool ok = p != nullptr && live;
+        uint32_t v = E == 4 ? ld_word((ok ? p : any_row) + off, io) : ld_half((ok ? p : any_row) + off, io);
+        v = ok ? v : 0u;
 #ifdef RS_MONO_SKIP_IO
-        p = nullptr;
         v = r * 0x9E3779B9u + off;
 #endif
-        if (p && live) v = E == 4 ? ld_word(p + off, io) : ld_half(p + off, io);
         w[j] = v;
     });
 }
@@ -697,9 +712,9 @@ struct ScaleTabs {
     uint32_t t[1 << LR][Fmt<E>::kTW];
     uint32_t erased;  // bit i: register i's row is not received
 };
-template <int L, int LR, bool SPLIT = false, int E = 4>
+template <int L, int LR, int SPLIT = 0, int E = 4>
 __device__ __forceinline__ void scale_issue(const MonoArgs &A, const uint32_t *rowinfo, ScaleTabs<L, LR, E> &st,
-                                            uint32_t lane, uint32_t wave) {
+                                            uint32_t lane, uint32_t wave, bool gather = true) {
     constexpr uint32_t PC = Fmt<E>::kPC;
     using S = SeqOf<L, LR, false, SPLIT>;
     const uint32_t a = lane_rows<S, 0>(lane, wave);
@@ -712,15 +727,12 @@ __device__ __forceinline__ void scale_issue(const MonoArgs &A, const uint32_t *r
         lg = 0;
 #endif
         st.erased |= ((f >> 16) & 1u) << i;
-#ifndef RS_MONO_SCALE_ALL_LANES
-        // only received rows gather a table (finish_col zeroes the others): lanes
-        // that load nothing return no bytes, so a 1 % decode's rows that are not
-        // received -- half the work rows -- cost no load bandwidth
-        if (!(f & 0x10000u))
-#else
-        if (f & 0x10000u) lg = 0;  // (the others read one shared table)
-#endif
-        {
+        // rows that are not received read one shared table (log 0: one cache
+        // line per instruction; finish_col zeroes those rows), so the gathers
+        // are unconditional and the waits for the table staging loads issued
+        // before them stay exact (see issue_col)
+        if (f & 0x10000u) lg = 0;
+        if (gather) {  // (wave-uniform: a wave with no received row skips them)
             const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + lg * PC;
 #pragma unroll
             for (int v = 0; v < int(PC); ++v) {
@@ -768,7 +780,7 @@ __device__ __forceinline__ void load_col(const MonoArgs &A, uint32_t chunk, cons
 // Store transform rows `chunk * n + row` that fall in A.dst (placement: end
 // of the FFT), paired like the loads.  REVEAL (decode): only erased rows,
 // multiplied by exp(65535 - log factor) (rate_high.rs:241-245).
-template <int L, int LR, bool REVEAL, bool SPLIT = false, int E = 4>
+template <int L, int LR, bool REVEAL, int SPLIT = 0, int E = 4>
 __device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *rowinfo, uint32_t chunk,
                                           const PackIO &io, const StripeBases &sb, Col<L, LR, E> &c, uint32_t lane,
                                           uint32_t wave) {
@@ -1120,9 +1132,18 @@ __device__ __forceinline__ void col_walsh(uint32_t (&x)[2], uint32_t *buf) {
 // rinfo[r] = log factor | (received ? 0 : 0x10000) for the 2^L work rows.
 // ebits / rbits: this thread's erased / received bits (bits 0, 1 = rows 2t,
 // 2t+1); lw: lw_fold of those rows.  Ends with a barrier.
-template <int L>
-__device__ __forceinline__ void col_eval_poly(const MonoArgs &A, uint32_t ebits, uint32_t rbits,
-                                              const uint32_t (&lw)[2], uint32_t *buf, uint32_t *rinfo) {
+// s_waitcnt vmcnt(N) (a load the compiler does not track: see mono_body)
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// lwv: the thread's lw_fold pair (rows 2t, 2t + 1), loaded by inline asm with
+// NLIVE vector loads issued after it (NSKIP in a wave with `skip`).
+template <int L, int NLIVE, int NSKIP>
+__device__ __forceinline__ void col_eval_poly(const MonoArgs &A, uint32_t ebits, uint32_t rbits, uint32_t lwv,
+                                              bool skip, uint32_t *buf, uint32_t *rinfo) {
     const uint32_t i0 = 2 * threadIdx.x;
     uint32_t x[2];
     static_for<0, 2>([&](auto kc) {
@@ -1132,6 +1153,11 @@ __device__ __forceinline__ void col_eval_poly(const MonoArgs &A, uint32_t ebits,
         x[k] = A.low_rate ? (i < A.end ? (e ? 0u : 65534u) : 0u) : e;
     });
     col_walsh<L>(x, buf);
+    RS_MSTAMP(14);
+    if (skip) vm_wait<NSKIP>();
+    else vm_wait<NLIVE>();
+    RS_MSTAMP(15);
+    const uint32_t lw[2] = {lwv & 0xFFFFu, lwv >> 16};
     static_for<0, 2>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
         const uint32_t p = x[k] * lw[k];
@@ -1150,7 +1176,7 @@ __device__ __forceinline__ void col_eval_poly(const MonoArgs &A, uint32_t ebits,
 // LDS staging of the twiddle tables (STAGED kernel): 16-byte pieces q of the
 // wave-private region (phase 1 from the IFFT image, phase 3 from the FFT
 // image) and of the shared region.
-template <int L, int LR, bool SPLIT, int E>
+template <int L, int LR, int SPLIT, int E>
 __device__ __forceinline__ uint4 priv_piece(const uint32_t *img, uint32_t wave, uint32_t q) {
     using G = Stage<L, LR, SPLIT, E>;
     const uint32_t t = q / G::PC, piece = q - t * G::PC;
@@ -1162,27 +1188,36 @@ __device__ __forceinline__ uint4 priv_piece(const uint32_t *img, uint32_t wave, 
 }
 // 16-byte piece q of the layer-0 tables of wave `wave`'s phase-1 / -3 rows
 // (image slots wave * W/2 .. : contiguous, one coalesced read per wave)
-template <int L, int LR, bool SPLIT, int E>
+template <int L, int LR, int SPLIT, int E>
 __device__ __forceinline__ uint4 l0_piece(const uint32_t *img, uint32_t wave, uint32_t q) {
     using G = Stage<L, LR, SPLIT, E>;
     return reinterpret_cast<const uint4 *>(img)[wave * G::kL0 * G::PC + q];
 }
-template <int L, int LR, bool SPLIT, int E>
-__device__ __forceinline__ uint4 shared_piece(const uint32_t *img_i, const uint32_t *img_f, uint32_t q) {
+template <int L, int LR, int SPLIT, int E>
+__device__ __forceinline__ const uint4 *shared_piece_ptr(const uint32_t *img_i, const uint32_t *img_f, uint32_t q) {
     using G = Stage<L, LR, SPLIT, E>;
     const uint32_t t = q / G::PC, piece = q - t * G::PC;
-    const uint32_t slot = t < G::kShI ? G::n - (G::n >> G::IW) + t : G::n - (G::n >> G::WB) + (t - G::kShI);
-    return reinterpret_cast<const uint4 *>(t < G::kShI ? img_i : img_f)[slot * G::PC + piece];
+    const uint32_t slot = t < G::kShI ? G::n - (G::n >> G::IW) + t : G::n - (G::n >> G::FLO) + (t - G::kShI);
+    return reinterpret_cast<const uint4 *>(t < G::kShI ? img_i : img_f) + slot * G::PC + piece;
 }
 // 16-byte piece q of the D tables (Stage::kD): layer b = q / PC of image t_i ^ t_f, group 0
-template <int L, int LR, bool SPLIT, int E>
-__device__ __forceinline__ uint4 d_piece(const uint32_t *img_d, uint32_t q) {
+template <int L, int LR, int SPLIT, int E>
+__device__ __forceinline__ const uint4 *d_piece_ptr(const uint32_t *img_d, uint32_t q) {
     using G = Stage<L, LR, SPLIT, E>;
     const uint32_t b = q / G::PC, piece = q - b * G::PC;
-    return reinterpret_cast<const uint4 *>(img_d)[(G::n - (G::n >> b)) * G::PC + piece];
+    return reinterpret_cast<const uint4 *>(img_d) + (G::n - (G::n >> b)) * G::PC + piece;
 }
+// one 16-byte piece as a value (a struct copy `x = *p` becomes a memcpy that
+// can keep the destination array in scratch)
+__device__ __forceinline__ uint4 ld_piece(const uint4 *p) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u v = *reinterpret_cast<const v4u *>(p);
+    return uint4{v.x, v.y, v.z, v.w};
+}
+// a staging lane's piece index, clamped into the region's [0, count) (count >= 1)
+__device__ __forceinline__ uint32_t clamp_piece(uint32_t q, uint32_t count) { return q < count ? q : count - 1u; }
 // layer of table slot t of a wave-private region (phases 1 and 3)
-template <int L, int LR, bool SPLIT, int E>
+template <int L, int LR, int SPLIT, int E>
 __device__ __forceinline__ uint32_t priv_layer(uint32_t t) {
     using G = Stage<L, LR, SPLIT, E>;
     const uint32_t y = (G::W >> G::B0) - t;
@@ -1193,10 +1228,94 @@ __device__ __forceinline__ uint32_t priv_layer(uint32_t t) {
 #define RS_MONO_LDS_PF 2
 #endif
 
+// plan kind of a kernel variant (Plan's SP): bit 0 split, bit 1 FLOW (the
+// staged decodes, unless RS_MONO_NO_FLOW)
+constexpr int mono_pk(int mode, bool staged, bool split) {
+#ifndef RS_MONO_NO_FLOW
+    const bool flow = staged && mode == kMonoDecode;
+#else
+    const bool flow = false;
+#endif
+    return (split ? 1 : 0) | (flow ? 2 : 0);
+}
+
+// Kernel arguments held in SGPRs from the kernel's start: the compiler treats
+// argument loads as re-loadable and re-issues them next to later uses (one
+// serialized scalar round trip each, a dozen of them ahead of the first row
+// load).  All of them are loaded first, then pass through one empty asm that
+// makes them values the compiler cannot reload; pointers pass as global
+// (address space 1) pointers, so accesses through them stay global_* (not flat).
+template <typename T>
+using gptr = __attribute__((address_space(1))) T *;
+template <typename T>
+__device__ __forceinline__ gptr<T> as_global(T *p) {
+    return (gptr<T>)p;
+}
+
 template <int L, int LR, int MODE, bool STAGED, bool BATCH, bool SPLIT, int E>
-__device__ __forceinline__ void mono_body(const MonoArgs &A) {
+__device__ __forceinline__ void mono_body(const MonoArgs &K) {
+    MonoArgs A;  // the scalar arguments; the erasure bitmaps stay in K
+    uint32_t ew[4] = {0, 0, 0, 0}, rw[4] = {0, 0, 0, 0};  // staged decode: the wave's bitmap words
+    {
+        uint32_t packs = K.packs, ppx = K.packs_per_xcd, nsrc = K.nsrc;
+        gptr<const uint8_t> b0 = as_global(K.src[0].base), b1 = as_global(K.src[1].base);
+        gptr<const uint8_t> bd = as_global(K.dst.base);
+        uint64_t st0 = K.src[0].stride, st1 = K.src[1].stride, std_ = K.dst.stride;
+        uint32_t rb0 = K.src[0].row_begin, re0 = K.src[0].row_end, rb1 = K.src[1].row_begin, re1 = K.src[1].row_end;
+        uint32_t rbd = K.dst.row_begin, red = K.dst.row_end;
+        gptr<const uint32_t> img = as_global(K.img), lut = as_global(K.lut);
+        gptr<const uint16_t> lwf = as_global(K.lw_fold);
+        uint32_t ii = K.ifft_img, fi = K.fft_img, fp = K.fmt.full_packs, th = K.fmt.tail_h, iob = K.fmt.io_bytes;
+        uint32_t lowr = K.low_rate, endr = K.end, lw0 = K.lw0, oh = K.out_half;
+        uint64_t imw = K.img_words;
+        if constexpr (STAGED && MODE == kMonoDecode) {  // this wave's words of the erasure bitmaps
+            const uint32_t w4 = 4u * __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            static_for<0, 4>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                ew[i] = K.erased[w4 + i];
+                rw[i] = K.received[w4 + i];
+            });
+        }
+        asm volatile("" : "+s"(packs), "+s"(ppx), "+s"(nsrc), "+s"(b0), "+s"(b1), "+s"(bd), "+s"(st0), "+s"(st1),
+                     "+s"(std_), "+s"(rb0), "+s"(re0), "+s"(rb1), "+s"(re1), "+s"(rbd), "+s"(red), "+s"(img),
+                     "+s"(lut), "+s"(lwf), "+s"(ii), "+s"(fi), "+s"(fp), "+s"(th), "+s"(iob), "+s"(lowr),
+                     "+s"(endr), "+s"(lw0), "+s"(oh), "+s"(imw), "+s"(ew[0]), "+s"(ew[1]), "+s"(ew[2]), "+s"(ew[3]),
+                     "+s"(rw[0]), "+s"(rw[1]), "+s"(rw[2]), "+s"(rw[3]));
+        A.img_words = imw;
+        A.packs = packs;
+        A.packs_per_xcd = ppx;
+        A.nsrc = nsrc;
+        A.src[0] = RowMap{(const uint8_t *)b0, st0, rb0, re0};
+        A.src[1] = RowMap{(const uint8_t *)b1, st1, rb1, re1};
+        A.dst = RowMap{(const uint8_t *)bd, std_, rbd, red};
+        A.img = (const uint32_t *)img;
+        A.lut = (const uint32_t *)lut;
+        A.lw_fold = (const uint16_t *)lwf;
+        A.ifft_img = ii;
+        A.fft_img = fi;
+        A.fmt = ShardFormat{fp, th, iob};
+        A.low_rate = lowr;
+        A.end = endr;
+        A.lw0 = lw0;
+        A.out_half = oh;
+    }
+    A.chunks = K.chunks;
+    A.elems = K.elems;
+    A.ifft_img_step = K.ifft_img_step;
+    A.fft_img_step = K.fft_img_step;
+    A.rowinfo = K.rowinfo;
+    A.fused_eval = K.fused_eval;
+    A.split = K.split;
+    A.stripes = K.stripes;
+    if constexpr (BATCH) {
+        A.src_bstride[0] = K.src_bstride[0];
+        A.src_bstride[1] = K.src_bstride[1];
+        A.dst_bstride = K.dst_bstride;
+    }
     using C = Col<L, LR, E>;
-    using G = Stage<L, LR, SPLIT, E>;
+    // plan kind: split; FLOW for the staged decodes (Plan)
+    constexpr int PK = mono_pk(MODE, STAGED, SPLIT);
+    using G = Stage<L, LR, PK, E>;
     static_assert(!SPLIT || (STAGED && MODE == kMonoDecode), "split plan: staged decode only");
     static_assert(STAGED || E == 4, "2-element packs: staged kernel only");
     constexpr int R = 1 << LR;
@@ -1242,10 +1361,8 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
         // rows and no phase-1 tables, and skips the phase-1 layers
         bool live = true;
         if constexpr (DEC) {
-            constexpr uint32_t kWords = (1u << G::IW) / 32;
-            uint32_t any = 0;
-            static_for<0, kWords>([&](auto kc) { any |= A.received[wave * kWords + decltype(kc)::value]; });
-            live = any != 0;
+            static_assert(!STAGED || (1u << G::IW) / 32 == 4, "a wave's phase-1 rows: its 4 bitmap words");
+            live = (rw[0] | rw[1] | rw[2] | rw[3]) != 0;
         }
         // split decode: does this wave's half go on with the FFT (restored rows)?
         const bool out_wave = !SPLIT || (wave >> (L - 1 - G::IW)) == A.out_half;
@@ -1261,56 +1378,122 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
         const bool reuse3 = false;
 #endif
 
-        // every global read is requested before any of them is waited for
-        // (no branches between them: a branch would make the compiler wait)
-        uint32_t ebits = 0, rbits = 0, lw[2] = {0, 0};
+        // every global read is requested before any of them is waited for.
+        // Decodes: eval_poly's inputs first.  Thread t's erased / received bits
+        // (rows 2t, 2t + 1) are in word t / 16 of the bitmaps: the wave's 4 words
+        // are uniform, i.e. scalar loads of the kernel arguments.  Its lw_fold
+        // pair is the first vector load, issued by inline asm, so the compiler's
+        // vmcnt waits do not know it: col_eval_poly waits for it by an explicit
+        // count of the vector loads issued after it (rows and table pieces, all
+        // unconditional), leaving those in flight while eval_poly runs
+        uint32_t ebits = 0, rbits = 0, lwv = 0;
         if constexpr (DEC) {  // the staged decode always evaluates eval_poly itself
-            const uint32_t i0 = 2 * threadIdx.x;
-            ebits = A.erased[i0 >> 5] >> (i0 & 31);
-            rbits = A.received[i0 >> 5] >> (i0 & 31);
-            lw[0] = A.lw_fold[i0];
-            lw[1] = A.lw_fold[i0 + 1];
+            const uint32_t g = lane >> 4, sh = (2u * lane) & 31u;
+            const uint32_t e0 = ew[0], e1 = ew[1], e2 = ew[2], e3 = ew[3], r0 = rw[0], r1 = rw[1], r2 = rw[2], r3 = rw[3];
+            ebits = (g == 0 ? e0 : g == 1 ? e1 : g == 2 ? e2 : e3) >> sh;
+            rbits = (g == 0 ? r0 : g == 1 ? r1 : g == 2 ? r2 : r3) >> sh;
+            // (lw_fold + 2t: 2-byte aligned; the compiler's own merged loads of it
+            // are the same unaligned dword access)
+            asm volatile("global_load_dword %0, %1, off" : "=v"(lwv) : "v"(A.lw_fold + 2u * threadIdx.x) : "memory");
         }
-        uint32_t w[2 << LR];
-        issue_col<L, LR, SPLIT, E>(A, 0, io, sb, w, lane, wave, live);
-        // phase-1 tables (a wave that skips phase 1 reads one table: no branch
-        // around the loads); B0: layer 0's go into the region first, the
+        // Decodes: a wave whose phase-1 rows hold no received row (!live) loads
+        // no rows, no phase-1 tables and no scale tables (uniform branches: the
+        // vector-memory issue rate of the ~330 load instructions of a 2^11-row
+        // workgroup bounds the prologue, and 7 of 16 waves are not live at 1 %)
+#ifndef RS_MONO_DEC_LOAD_ALL
+        const bool skip = DEC && !live;
+#else
+        const bool skip = false;
+#endif
+        uint32_t w[2 << LR] = {};
+        auto issue_rows = [&]() { issue_col<L, LR, PK, E>(A, 0, io, sb, w, lane, wave, live); };
+        // phase-1 tables (a live wave loads all of its region's pieces; lanes past
+        // the region's end re-read its last piece and do not write it, so the
+        // loads are unconditional); B0: layer 0's go into the region first, the
         // layers above when layer 0 has read them (run_seq's hook)
         uint4 v0[KP0], v1[KP1], vs[KSH];
+        auto issue_priv = [&]() {
 #ifndef RS_MONO_SKIP_STAGE  // tools/mono_probe.hip ablation
-        if constexpr (G::B0)
-            static_for<0, KP0>([&](auto kc) {
-                const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < PC * G::kL0) v0[kc] = l0_piece<L, LR, SPLIT, E>(img_i, wave, live ? q : q % PC);
+            if constexpr (G::B0)
+                static_for<0, KP0>([&](auto kc) {
+                    const uint32_t q = clamp_piece(lane + 64u * decltype(kc)::value, PC * G::kL0);
+                    v0[kc] = l0_piece<L, LR, PK, E>(img_i, wave, live ? q : q % PC);
+                });
+            static_for<0, KP1>([&](auto kc) {
+                const uint32_t q = clamp_piece(lane + 64u * decltype(kc)::value, PC * G::kUp);
+                v1[kc] = priv_piece<L, LR, PK, E>(img_i, wave, live ? q : q % PC);
             });
-        static_for<0, KP1>([&](auto kc) {
-            const uint32_t q = lane + 64u * decltype(kc)::value;
-            if (q < PC * G::kUp) v1[kc] = priv_piece<L, LR, SPLIT, E>(img_i, wave, live ? q : q % PC);
-        });
-        static_for<0, KSH>([&](auto kc) {
-            const uint32_t q = threadIdx.x + T * decltype(kc)::value;
-            if (q < PC * G::kShared) vs[kc] = shared_piece<L, LR, SPLIT, E>(img_i, img_f, q);
-            else if (!DEC && q < PC * kSh) vs[kc] = d_piece<L, LR, SPLIT, E>(img_d, q - PC * G::kShared);
-        });
 #endif
+        };
+        // the shared region: every thread of the workgroup loads and writes pieces
+        auto issue_shared = [&]() {
+#ifndef RS_MONO_SKIP_STAGE
+            if constexpr (kSh > 0)
+                static_for<0, KSH>([&](auto kc) {
+                    const uint32_t q = clamp_piece(threadIdx.x + T * decltype(kc)::value, PC * kSh);
+                    if constexpr (kSh == G::kShared) {
+                        vs[kc] = ld_piece(shared_piece_ptr<L, LR, PK, E>(img_i, img_f, q));
+                    } else {
+                        const uint4 *src = q < PC * G::kShared ? shared_piece_ptr<L, LR, PK, E>(img_i, img_f, q)
+                                                               : d_piece_ptr<L, LR, PK, E>(img_d, q - PC * G::kShared);
+                        vs[kc] = ld_piece(src);
+                    }
+                });
+#endif
+        };
+#ifndef RS_MONO_SKIP_STAGE
+        constexpr int kPrivLoads = (G::B0 ? KP0 : 0) + KP1, kShLoads = kSh > 0 ? KSH : 0;
+#else
+        constexpr int kPrivLoads = 0, kShLoads = 0;
+#endif
+        constexpr int kRowLoads = 2 << LR;
+        // Decodes, order of the loads around eval_poly (inputs first, see above).
+        // RS_MONO_DEC_ORDER 1: the shared tables, the live waves' rows and phase-1
+        // tables, all in flight while eval_poly runs, then the scale gathers;
+        // 2: rows, eval_poly, gathers, then the tables; 3: shared tables and rows,
+        // eval_poly, gathers, phase-1 tables
+#ifndef RS_MONO_DEC_ORDER
+#define RS_MONO_DEC_ORDER 1
+#endif
+        constexpr int kOrder = RS_MONO_DEC_ORDER;
+        constexpr bool kShFirst = kOrder != 2, kPrivFirst = kOrder == 1;
+        if constexpr (!DEC) {
+            issue_rows();
+            issue_priv();
+            issue_shared();
+        } else {
+            if constexpr (kShFirst) issue_shared();
+            if (!skip) {
+                issue_rows();
+                if constexpr (kPrivFirst) issue_priv();
+            }
+        }
         const uint32_t *ri = A.rowinfo;
         if constexpr (DEC) {
+            // vector loads issued after lw_fold's (see above), per branch
+            constexpr int kAfterSkip = kShFirst ? kShLoads : 0;
+            constexpr int kAfterLive = kAfterSkip + kRowLoads + (kPrivFirst ? kPrivLoads : 0);
 #ifndef RS_MONO_SKIP_EVAL  // tools/mono_probe.hip ablation
-            col_eval_poly<L>(A, ebits, rbits, lw, plane, rinfo);
+            col_eval_poly<L, kAfterLive, kAfterSkip>(A, ebits, rbits, lwv, skip, plane, rinfo);
 #else
-            rinfo[2 * threadIdx.x] = ebits & 1u ? 0x10000u : lw[0];
-            rinfo[2 * threadIdx.x + 1] = ebits & 2u ? 0x10000u : lw[1];
+            if (skip) vm_wait<kAfterSkip>();
+            else vm_wait<kAfterLive>();
+            rinfo[2 * threadIdx.x] = ebits & 1u ? 0x10000u : lwv & 0xFFFFu;
+            rinfo[2 * threadIdx.x + 1] = ebits & 2u ? 0x10000u : lwv >> 16;
             __syncthreads();
 #endif
             ri = rinfo;
             RS_MSTAMP(2);
         }
         ScaleTabs<L, LR, E> st;
-        // (decodes) every load issued so far -- rows, tables, eval_poly's inputs --
-        // has landed while eval_poly ran; saying so here lets the table writes
-        // below go ahead without waiting for the (lane-conditional) scale gathers
-        if constexpr (DEC) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-        if constexpr (DEC) scale_issue<L, LR, SPLIT, E>(A, ri, st, lane, wave);
+        // (decodes) the scale gathers go out as soon as eval_poly is done
+        if constexpr (DEC) {
+            scale_issue<L, LR, PK, E>(A, ri, st, lane, wave, !skip);
+            if constexpr (!kShFirst) issue_shared();
+            if constexpr (!kPrivFirst)
+                if (!skip) issue_priv();
+        }
+        RS_MSTAMP(13);
         auto write1 = [&]() {
 #ifndef RS_MONO_SKIP_STAGE
             static_for<0, KP1>([&](auto kc) {
@@ -1320,30 +1503,33 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
 #endif
         };
 #ifndef RS_MONO_SKIP_STAGE
-        if constexpr (G::B0)
-            static_for<0, KP0>([&](auto kc) {
-                const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at0(q)] = v0[kc];
-            });
-        else
-            write1();
+        if (!skip) {  // (a skipping wave's region is written by phase 3's tables before use)
+            if constexpr (G::B0)
+                static_for<0, KP0>([&](auto kc) {
+                    const uint32_t q = lane + 64u * decltype(kc)::value;
+                    if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at0(q)] = v0[kc];
+                });
+            else
+                write1();
+        }
         static_for<0, KSH>([&](auto kc) {
             const uint32_t q = threadIdx.x + T * decltype(kc)::value;
             if (q < PC * kSh) reinterpret_cast<uint4 *>(shared)[G::atS(q)] = vs[kc];
         });
 #endif
-        RS_MSTAMP(6);
         finish_col<L, LR, DEC>(w, &st, c, lane);
         RS_MSTAMP(1);
-        const LdsTabs<L, LR, SPLIT, E> ts{priv, shared, img_i, img_f};
+        const LdsTabs<L, LR, PK, E> ts{priv, shared, img_i, img_f};
         // phase-3 tables: requested when phase 1 ends, written over this wave's
         // phase-1 tables when phase 2 ends
         uint4 v3[KP3];
         auto issue3 = [&]() {
             if (reuse3) return;
+            if constexpr (G::kP3 > 0)
             static_for<0, KP3>([&](auto kc) {
                 const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < PC * G::kP3) v3[kc] = priv_piece<L, LR, SPLIT, E>(img_f, wave, out_wave ? q : q % PC);
+                const uint32_t qc = clamp_piece(q, PC * G::kP3);
+                v3[kc] = priv_piece<L, LR, PK, E>(img_f, wave, out_wave ? qc : qc % PC);
             });
         };
         auto write3 = [&]() {
@@ -1356,7 +1542,7 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
                         if (q < PC * G::kP3) {
                             const uint32_t t = q / PC, piece = q - t * PC;
                             const uint4 v = reinterpret_cast<const uint4 *>(priv)[G::at1(q)];
-                            const uint4 d = reinterpret_cast<const uint4 *>(shared)[(G::kShared + priv_layer<L, LR, SPLIT, E>(t)) * G::SPC + piece];
+                            const uint4 d = reinterpret_cast<const uint4 *>(shared)[(G::kShared + priv_layer<L, LR, PK, E>(t)) * G::SPC + piece];
                             x[kc] = uint4{v.x ^ d.x, v.y ^ d.y, v.z ^ d.z, v.w ^ d.w};
                         }
                     });
@@ -1379,7 +1565,8 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
             if constexpr (G::B0)
                 static_for<0, KP0>([&](auto kc) {
                     const uint32_t q = lane + 64u * decltype(kc)::value;
-                    if (q < PC * G::kL0) v4[kc] = l0_piece<L, LR, SPLIT, E>(img_f, wave, need ? q : q % PC);
+                    const uint32_t qc = clamp_piece(q, PC * G::kL0);
+                    v4[kc] = l0_piece<L, LR, PK, E>(img_f, wave, need ? qc : qc % PC);
                 });
         };
         auto write4 = [&]() {
@@ -1394,45 +1581,47 @@ __device__ __forceinline__ void mono_body(const MonoArgs &A) {
             constexpr uint32_t kHalfWords = (G::n / 2) / 32;
             uint32_t half_any = 0;
             const uint32_t h = wave >> (L - 1 - G::IW);
-            for (uint32_t k = 0; k < kHalfWords; ++k) half_any |= A.received[h * kHalfWords + k];
+            for (uint32_t k = 0; k < kHalfWords; ++k) half_any |= K.received[h * kHalfWords + k];
             // IFFT: a wave whose rows hold no received row skips phase 1 (its rows
             // stay zero), a half without received rows skips phase 2
-            run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 1 : -1, true>(ts, c, plane, lane, wave, issue3,
+            run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 1 : -1, PK>(ts, c, plane, lane, wave, issue3,
                                                                          half_any != 0, live, write1);
-            using SF = SeqOf<L, LR, true, true>;
+            RS_MSTAMP(5);
+            using SF = SeqOf<L, LR, true, PK>;
             constexpr int NLF = num_layers(SF::v);
             const bool out = out_wave;
-            const bool alive = out && wave_stores<L, LR, true>(A, wave);
-            constexpr uint32_t kTopI = (G::n >> G::IW) - 2, kTopF = G::kShI + (G::n >> G::WB) - 2;
+            const bool alive = out && wave_stores<L, LR, PK>(A, wave);
+            constexpr uint32_t kTopI = (G::n >> G::IW) - 2, kTopF = G::kShI + (G::n >> G::FLO) - 2;
             split_top<L, LR>(c, plane, lds + G::words_dec, shared + kTopI * G::SW, shared + kTopF * G::SW, lane, wave,
                              A.out_half);
+            RS_MSTAMP(6);
             issue4(alive);
             // FFT below the top layer: only the half that holds restored rows
-            run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, true>(ts, c, plane, lane, wave, write3, alive,
+            run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, PK>(ts, c, plane, lane, wave, write3, alive,
                                                                               out, write4);
             if (!alive) return;
         } else if constexpr (G::WB > 0) {
-            run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 1 : -1>(ts, c, plane, lane, wave, issue3, true, live,
+            run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 1 : -1, PK>(ts, c, plane, lane, wave, issue3, true, live,
                                                                    write1);
             RS_MSTAMP(5);
-            using SF = SeqOf<L, LR, true>;
+            using SF = SeqOf<L, LR, true, PK>;
             constexpr int NLF = num_layers(SF::v);
-            const bool alive = !DEC || wave_stores<L, LR>(A, wave);
+            const bool alive = !DEC || wave_stores<L, LR, PK>(A, wave);
             issue4(alive);  // (waves that stop early all read one table: no branch around the loads)
             if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
-            run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1>(ts, c, plane, lane, wave, write3, alive, true,
+            run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, PK>(ts, c, plane, lane, wave, write3, alive, true,
                                                                         write4);
             if (!alive) return;
         } else {
             static_assert(!G::B0, "one-segment plans keep every table in the region");
-            run_seq<L, LR, false, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, NoHook{});
+            run_seq<L, LR, false, RS_MONO_LDS_PF, -1, PK>(ts, c, plane, lane, wave, NoHook{});
             issue3();
             if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
             write3();
-            run_seq<L, LR, true, RS_MONO_LDS_PF>(ts, c, plane, lane, wave, NoHook{});
+            run_seq<L, LR, true, RS_MONO_LDS_PF, -1, PK>(ts, c, plane, lane, wave, NoHook{});
         }
         RS_MSTAMP(10);
-        store_col<L, LR, DEC, SPLIT>(A, ri, 0, io, sb, c, lane, wave);
+        store_col<L, LR, DEC, PK>(A, ri, 0, io, sb, c, lane, wave);
         RS_MSTAMP(11);
     } else if constexpr (MODE == kMonoEncodeHigh) {
         // rate_high.rs:44-87: recovery = FFT_0(XOR_c IFFT_{c n + n}(chunk c))
@@ -1494,7 +1683,7 @@ constexpr int mono_lr(int L, bool staged) {
 template <int L, int MODE, bool STAGED, bool BATCH = false, bool SPLIT = false, int E = 4>
 hipError_t launch_ls(const MonoArgs &A, hipStream_t s) {
     constexpr int LR = mono_lr(L, STAGED);
-    using G = Stage<L, LR, SPLIT, E>;
+    using G = Stage<L, LR, mono_pk(MODE, STAGED, SPLIT), E>;
     size_t lds = STAGED ? size_t(SPLIT ? G::words_split : MODE == kMonoDecode ? G::words_dec : G::words_enc) * 4
                         : size_t(8) << L;
     // 2-element packs exist to spread a launch over more CUs: more than half the
@@ -1541,17 +1730,32 @@ hipError_t launch_l(const MonoArgs &A, hipStream_t s) {
     return launch_ls<L, MODE, false>(A, s);
 }
 
+// RS_MONO_ONLY_L / RS_MONO_ONLY_MODE (development probes, tools/): build the
+// kernels of one transform size / one mode only (compile time)
+#ifdef RS_MONO_ONLY_L
+#define RS_MONO_HAS_L(l) ((l) == RS_MONO_ONLY_L)
+#else
+#define RS_MONO_HAS_L(l) true
+#endif
+#ifdef RS_MONO_ONLY_MODE
+#define RS_MONO_HAS_MODE(m) ((m) == RS_MONO_ONLY_MODE)
+#else
+#define RS_MONO_HAS_MODE(m) true
+#endif
+
 template <int MODE>
 hipError_t launch_m(int L, const MonoArgs &A, hipStream_t s) {
+    if constexpr (!RS_MONO_HAS_MODE(MODE)) return hipErrorNotSupported;
     switch (L) {
-        case 7: return launch_l<7, MODE>(A, s);
-        case 8: return launch_l<8, MODE>(A, s);
-        case 9: return launch_l<9, MODE>(A, s);
-        case 10: return launch_l<10, MODE>(A, s);
-        case 11: return launch_l<11, MODE>(A, s);
-        case 12: return launch_l<12, MODE>(A, s);
-        default: return hipErrorNotSupported;
+        case 7: if constexpr (RS_MONO_HAS_L(7)) return launch_l<7, MODE>(A, s); break;
+        case 8: if constexpr (RS_MONO_HAS_L(8)) return launch_l<8, MODE>(A, s); break;
+        case 9: if constexpr (RS_MONO_HAS_L(9)) return launch_l<9, MODE>(A, s); break;
+        case 10: if constexpr (RS_MONO_HAS_L(10)) return launch_l<10, MODE>(A, s); break;
+        case 11: if constexpr (RS_MONO_HAS_L(11)) return launch_l<11, MODE>(A, s); break;
+        case 12: if constexpr (RS_MONO_HAS_L(12)) return launch_l<12, MODE>(A, s); break;
+        default: break;
     }
+    return hipErrorNotSupported;
 }
 
 }  // namespace

@@ -5,7 +5,11 @@
 #ifndef RS_MONO_NO_STAMPS
 #define RS_MONO_STAMPS 1
 #endif
+#ifdef RS_MONO_SRC  // A/B: another version of the kernel source (include path: csrc)
+#include RS_MONO_SRC
+#else
 #include "../reed-solomon-simd_amd/csrc/rs_mono.hip"
+#endif
 
 #include <algorithm>
 #include <string>
@@ -140,9 +144,10 @@ int main(int argc, char **argv) {
         }
         printf("entry spread within an XCD (worst XCD): %.2f us\n", sp);
     }
-    const char *names[16] = {"start", "loaded", "eval done", "ifft A done", "remap1 done", "ifft B done", "staged", "entry",
-                             "fft B done", "remap2 done", "fft C done", "stored", "entry wave0"};
-    const int order[] = {12, 7, 0, 2, 6, 1, 3, 4, 5, 8, 9, 10, 11};
+    const char *names[16] = {"start", "loaded", "eval done", "ifft A done", "remap1 done", "ifft B done", "split done", "entry",
+                             "fft B done", "remap2 done", "fft C done", "stored", "entry wave0", "loads issued",
+                             "walsh1 done", "lw landed"};
+    const int order[] = {12, 7, 0, 14, 15, 2, 13, 1, 3, 4, 5, 6, 8, 9, 10, 11};
     for (int i : order) {
         std::vector<double> v;
         for (uint32_t w = 0; w < wgs; ++w) v.push_back((double(st[w * 16 + i]) - double(st[w * 16 + 12])) * 0.01);
