@@ -73,6 +73,9 @@ def parse():
     p.add_argument("--batch", type=int, default=64, help="stripes per call of the batched measurement (1 = skip)")
     p.add_argument("--plumbing", action="store_true",
                    help="CPU/gloo check of the rank launcher and timing reduction (no GPU, no kernels)")
+    p.add_argument("--shape-table", action="store_true",
+                   help="time the reference README's shape table (README.md:27-45, 1 KiB shards): device "
+                        "encode and 1 %% / 100 %% decode, the route each takes, and the AVX2 port on one core")
     return p.parse_args()
 
 
@@ -151,6 +154,9 @@ def main():
     import reed_solomon_simd as rs
 
     ctx = rs.Context(local)
+    if args.shape_table:
+        shape_table(args, rs, ctx, torch.device("cuda", local))
+        return
     config = args.config or (SHARDED if world > 1 else HEADLINE)
     dev = torch.device("cuda", local)
     if config == SHARDED:
@@ -477,6 +483,92 @@ def sharded_bench(args, rs, ctx, world, rank, dev):
             "roofline": roofline,
             "cpu_baseline": cpu,
         }))
+
+
+# ---------------------------------------------------------------------------
+# --shape-table: the reference's published shape table (README.md:27-45)
+
+README_SHAPES = [(32, 32), (64, 64), (128, 128), (256, 256), (512, 512), (1024, 1024), (2048, 2048),
+                 (4096, 4096), (8192, 8192), (16384, 16384), (32768, 32768), (128, 1024), (1000, 100),
+                 (1000, 10000), (8192, 57344), (10000, 1000), (57344, 8192)]
+
+
+def _route(rs, ctx, fn):
+    """The kernels one call launches (rs_profile_enable records), e.g. 'k_mono<10, ...>' or the passes."""
+    import torch
+
+    rs.profile_enable(True, ctx=ctx)
+    fn()
+    torch.cuda.synchronize()
+    recs = rs.profile_collect(ctx)
+    rs.profile_enable(False, ctx=ctx)
+    return " + ".join(name for name, _, _ in recs)
+
+
+def _cpu_rate(fn, unit_bytes, seconds):
+    fn()
+    it, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        fn()
+        it += 1
+    return unit_bytes * it / (time.perf_counter() - t0) / 2**30
+
+
+def shape_table(args, rs, ctx, dev):
+    """Every shape of the reference's benchmark table (README.md:27-45) at 1 KiB shards: device-
+    resident encode and decode (1 % and 100 % original loss, the reference's pattern
+    benches/benchmarks.rs:113-138), wall time of `--steps` calls (at most 50) on one stream; the
+    route (kernels of one call); the AVX2 port (oracle/avx2_port.c) on one core, ≈0.2 s per
+    measurement.  GiB/s are of original + recovery bytes, as in the reference's table."""
+    import numpy as np
+    import torch
+    import oracle_lib as O
+
+    S = 1024
+    timed, _ = make_timer(1, dev)
+    stream = torch.cuda.Stream(device=dev)
+    steps = max(5, min(args.steps, 50))
+    cpu_ok = not args.no_cpu and O.lib().orc_select_engine(1) == 0
+    rows = []
+    for N, M in README_SHAPES:
+        g = torch.Generator(device=dev)
+        g.manual_seed(N * 7 + M)
+        d_orig = torch.randint(0, 256, (N, S), dtype=torch.uint8, device=dev, generator=g)
+        d_rec = torch.empty((M, S), dtype=torch.uint8, device=dev)
+        d_out = torch.empty((N, S), dtype=torch.uint8, device=dev)
+        enc = rs.encode_device_call(N, M, S, d_orig, d_rec, stream=stream, ctx=ctx)
+        step_bytes = (N + M) * S
+        row = {"shape": f"{N}:{M}", "rate": "high" if rs.use_high_rate(N, M) == 1 else "low"}
+        w = timed(enc, steps, 3)
+        row["encode_GiBps"] = round(step_bytes * steps / w / 2**30, 2)
+        row["encode_us"] = round(w / steps * 1e6, 2)
+        row["encode_route"] = _route(rs, ctx, enc)
+        enc()
+        torch.cuda.synchronize()
+        h_orig, h_rec = d_orig.cpu().numpy(), d_rec.cpu().numpy()
+        for pct in (1, 100):
+            L = -(-min(N, M) * pct // 100)
+            opf, rpf = [1] * (N - L) + [0] * L, [1] * L + [0] * (M - L)
+            dec = rs.decode_device_call(N, M, S, d_orig, rs.present_mask(opf), d_rec, rs.present_mask(rpf), d_out,
+                                        stream=stream, ctx=ctx)
+            w = timed(dec, steps, 3)
+            row[f"decode_{pct}pct_GiBps"] = round(step_bytes * steps / w / 2**30, 2)
+            row[f"decode_{pct}pct_us"] = round(w / steps * 1e6, 2)
+            if pct == 1:
+                row["decode_route"] = _route(rs, ctx, dec)
+            if cpu_ok:
+                row[f"cpu_decode_{pct}pct_GiBps"] = round(_cpu_rate(
+                    lambda: O.decode("default", h_orig, np.array(opf, np.uint8), h_rec, np.array(rpf, np.uint8)),
+                    step_bytes, 0.2), 3)
+        if cpu_ok:
+            row["cpu_encode_GiBps"] = round(_cpu_rate(lambda: O.encode("default", h_orig, M), step_bytes, 0.2), 3)
+        rows.append(row)
+        del d_orig, d_rec, d_out
+    if cpu_ok:
+        O.lib().orc_select_engine(0)
+    print(json.dumps({"metric": "shape table (README.md:27-45), 1 KiB shards, GiB/s of original + recovery",
+                      "steps": steps, "cpu": (f"AVX2 port, 1 thread, {_cpu_model()}" if cpu_ok else None),
+                      "rows": rows}))
 
 
 # ---------------------------------------------------------------------------

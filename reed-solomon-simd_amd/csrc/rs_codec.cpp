@@ -199,6 +199,7 @@ struct rs_context {
     // for encodes too when e2_encode (measured: tools/e2_probe.py)
     uint32_t e2_max_packs = 192;
     bool e2_encode = false;
+    int chunk_par = -1;           // RS_MI355X_CHUNK_PARALLEL: -1 by pack count (chunk_parallel), 0 / 1 forced
     uint32_t *d_lut2 = nullptr;   // perm2_by_log: the 2-element form of d_lut
     std::mutex img_mu;            // guards d_img, d_img2
     uint32_t *d_img[13] = {};     // column-kernel twiddle images per L (built at context creation)
@@ -467,6 +468,15 @@ void launch_mono(int mode, uint32_t L, const rs::MonoArgs &M, hipStream_t s, uin
     if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), bytes);
 }
 
+// Single-level multi-chunk encodes: spread the chunks over the grid (grid.y)
+// when the packs alone give few workgroups (RS_MI355X_CHUNK_PARALLEL = 0 / 1
+// forces the serial / parallel form; tools/ab_chunks.sh measures the threshold).
+constexpr uint32_t kChunkParallelMaxPacks = 4096;
+bool chunk_parallel(rs_context *ctx, const Geom &g) {
+    if (ctx->chunk_par >= 0) return ctx->chunk_par != 0;
+    return g.packs <= kChunkParallelMaxPacks;
+}
+
 // HighRate encode (rate_high.rs:44-87) from device rows to device rows:
 // chunk c's IFFT uses skew_delta c*n + n, the chunks are XOR-folded, one FFT
 // with skew_delta 0 produces the recovery rows.
@@ -500,7 +510,7 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
         launch_mono(rs::kMonoEncodeHigh, L, Mo, s, (N + M) * uint64_t(g.packs) * 8 * g.stripes);
         return;
     }
-    if (lv.m == 1) {
+    if (lv.m == 1 && (C == 1 || !chunk_parallel(ctx, g))) {
         A.src[0] = src;
         A.nsrc = 1;
         A.in_chunks = C;
@@ -509,6 +519,25 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
         return;
     }
     uint8_t *W = static_cast<uint8_t *>(ws.buf[0].get(size_t(C) * n * g.stride));
+    if (lv.m == 1) {
+        // one level, several chunks, few packs: every chunk's IFFT in its own
+        // workgroups (grid.y = chunk) into the work rows, then one pass XOR-folds
+        // the chunks and runs the FFT -- instead of one workgroup transforming
+        // the chunks one after another
+        A.work_stride = g.stride;
+        rs::PassArgs P = A;
+        P.grid_chunks = C;
+        P.src[0] = src;
+        P.nsrc = 1;
+        P.work_out = W;
+        run_level(P, lv, 0, rs::kIfft, n, s);
+        rs::PassArgs T = A;
+        T.work_in = W;
+        T.in_chunks = C;
+        T.dst = dst;
+        run_level(T, lv, 0, rs::kFft, n, s);
+        return;
+    }
     A.work_stride = g.stride;
     for (uint32_t k = 0; k + 1 < lv.m; ++k) {  // IFFT, low levels, every chunk
         rs::PassArgs P = A;
@@ -567,8 +596,17 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
     if (lv.m == 1) {
         A.src[0] = src;
         A.nsrc = 1;
-        A.out_chunks = C;
         A.dst = dst;
+        if (C > 1 && chunk_parallel(ctx, g)) {
+            // one level, several output chunks, few packs: each output chunk's
+            // workgroups (grid.y) run the IFFT of the originals themselves and that
+            // chunk's FFT -- instead of one workgroup running the chunks' FFTs one
+            // after another
+            A.grid_chunks = C;
+            A.in_chunk0 = 1;
+        } else {
+            A.out_chunks = C;
+        }
         run_level(A, lv, 0, rs::kIfft | rs::kFft, n, s);
         return;
     }
@@ -1084,6 +1122,7 @@ rs_status rs_context_create(int device, rs_context **out) {
         ctx->mono_all = ma && ma[0] == '1';
         if (const char *mp = getenv("RS_MI355X_MONO_MAX_PACKS")) ctx->mono_max_packs = uint32_t(strtoul(mp, nullptr, 10));
         if (const char *e2 = getenv("RS_MI355X_E2_MAX_PACKS")) ctx->e2_max_packs = uint32_t(strtoul(e2, nullptr, 10));
+        if (const char *cp = getenv("RS_MI355X_CHUNK_PARALLEL")) ctx->chunk_par = cp[0] == '1' ? 1 : 0;
         // column-kernel twiddle images of every transform size, built now: a lazy
         // build inside an asynchronous call would stall the device with a
         // synchronous upload the first time a size is seen

@@ -97,6 +97,7 @@ struct PassArgs {
     uint32_t packs = 0;    // packs per row (shard_bytes / 8)
     uint32_t slices = 0;   // ceil(packs / 64)
     uint32_t grid_chunks = 1;  // chunks spread over gridDim.y
+    uint32_t in_chunk0 = 0;    // rows load from chunk 0 whatever the grid's chunk (LowRate: one FFT per output chunk)
 
     // ---- load: transform row r = row(j) + chunk * n
     RowMap src[2];
@@ -162,7 +163,10 @@ char *launch_name_buf();
 // g * 2^(b+1) + 2^b + t * n - 1 at table slot n - n / 2^b + g.
 enum MonoMode { kMonoEncodeHigh = 0, kMonoEncodeLow = 1, kMonoDecode = 2 };
 constexpr uint32_t kMonoFusedRows = 2048;  // largest work size of the fused-eval_poly decode
-struct MonoArgs {
+// The kernel arguments of every column kernel; the staged decode's kernels take
+// MonoArgs (+ the erasure bitmaps), the others this core only: argument bytes
+// cost launch time (≈0.4 us per KiB back to back, tools/kernarg_probe.hip).
+struct MonoCore {
     uint32_t packs = 0;          // packs per row (shard_bytes / (2 * elems), rounded up)
     uint32_t packs_per_xcd = 0;  // ceil(packs / 8): workgroup b runs pack (b % 8) * packs_per_xcd + b / 8
     RowMap src[2];               // transform rows to load (others are zero)
@@ -177,20 +181,21 @@ struct MonoArgs {
     const uint32_t *rowinfo = nullptr;  // decode: bits 0-15 log factor, bit 16 erased
     const uint32_t *lut = nullptr;      // perm tables by log factor (Engine::mul semantics; format of elems)
     // decode with eval_poly fused into the staged kernel (every workgroup
-    // evaluates it; no rowinfo): erased / received bits of the 2^L work rows,
-    // as in EvalArgs
+    // evaluates it; no rowinfo; MonoArgs::erased / received)
     uint32_t fused_eval = 0, low_rate = 0, end = 0, lw0 = 0;
     // split plan (mono_split(L)): every restored row lies in half out_half of the 2^L work rows
     uint32_t split = 0, out_half = 0;
     ShardFormat fmt;  // byte layout of src / dst
     const uint16_t *lw_fold = nullptr;
-    uint32_t erased[kMonoFusedRows / 32] = {}, received[kMonoFusedRows / 32] = {};
     // a batch of stripes of one shape in one launch (staged kernel, grid.y =
     // stripes): stripe b's rows sit b * *_bstride bytes after the base
-    // pointers.  Last in the struct and read only by the batch instantiation,
-    // so the single-stripe kernel's argument loads stay as they were.
+    // pointers (read only by the batch instantiation)
     uint32_t stripes = 1;
     uint64_t src_bstride[2] = {0, 0}, dst_bstride = 0;
+};
+struct MonoArgs : MonoCore {
+    // fused-eval_poly decode: erased / received bits of the 2^L work rows, as in EvalArgs
+    uint32_t erased[kMonoFusedRows / 32] = {}, received[kMonoFusedRows / 32] = {};
 };
 // hipErrorNotSupported: no column kernel for this L (7 <= L <= 12 are built).
 hipError_t launch_mono(int mode, int L, const MonoArgs &A, hipStream_t stream);

@@ -667,7 +667,7 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
     uint32_t lo[P::R], hi[P::R];
     uint32_t xl[XOR_IN ? P::R : 1], xh[XOR_IN ? P::R : 1];
     // loads first, then table staging: one barrier covers both latencies
-    load_rows<K, LR, SPL, DO_IFFT ? 0 : PL, SCALE>(A, c, gchunk, lo, hi);
+    load_rows<K, LR, SPL, DO_IFFT ? 0 : PL, SCALE>(A, c, A.in_chunk0 ? 0u : gchunk, lo, hi);
     if constexpr (XOR_IN) load_xor_rows<K, LR, SPL, PL>(A, c, xl, xh);
     {
         auto st = stager_for<K, LR, SPL, FLAGS>(lds);
@@ -690,6 +690,14 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
                 transform<K, LR, SPL, true>(c, plane, tabI, tl, th);
                 static_for<0, P::R>([&](auto ic) { lo[ic] ^= tl[ic]; hi[ic] ^= th[ic]; });
             }
+        }
+    }
+    if constexpr (!DO_IFFT && MULTI_IN) {
+        // rows already transformed per chunk (work_in, one chunk after another): XOR-fold
+        for (uint32_t ci = 1; ci < A.in_chunks; ++ci) {
+            uint32_t tl[P::R], th[P::R];
+            load_rows<K, LR, SPL, PL, false>(A, c, gchunk + ci, tl, th);
+            static_for<0, P::R>([&](auto ic) { lo[ic] ^= tl[ic]; hi[ic] ^= th[ic]; });
         }
     }
     // rows are now in phase PL
@@ -767,6 +775,7 @@ hipError_t launch_k(int flags, const PassArgs &A, hipStream_t s) {
         case I | F | kMultiIn: return launch_f<K, LR, SPL, I | F | kMultiIn>(A, s);
         case I | F | kMultiOut: return launch_f<K, LR, SPL, I | F | kMultiOut>(A, s);
         case F | kMultiOut: return launch_f<K, LR, SPL, F | kMultiOut>(A, s);
+        case F | kMultiIn: return launch_f<K, LR, SPL, F | kMultiIn>(A, s);
         // decode: single pass, IFFT passes, fused top, FFT passes (middle / last)
         case I | F | kScale | kFd | kReveal: return launch_f<K, LR, SPL, I | F | kScale | kFd | kReveal>(A, s);
         case I | kScale: return launch_f<K, LR, SPL, I | kScale>(A, s);

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <type_traits>
 
 #include "rs_device.hpp"
 #include "rs_gf.hpp"
@@ -638,7 +639,7 @@ __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR, E> &c, uint32_t
 // Decode: does this wave hold, after the FFT's remap, any row of A.dst?
 // (there the wave's rows are one block of 2^IW consecutive rows)
 template <int L, int LR, int SPLIT = 0>
-__device__ __forceinline__ bool wave_stores(const MonoArgs &A, uint32_t wave) {
+__device__ __forceinline__ bool wave_stores(const MonoCore &A, uint32_t wave) {
     using S = SeqOf<L, LR, true, SPLIT>;
     constexpr int I = S::v.count;
     const uint32_t lo = lane_rows<S, I>(0, wave), hi = lo + (1u << (LR + 6));
@@ -650,12 +651,12 @@ struct StripeBases {
     const uint8_t *src0, *src1;
     uint8_t *dst;
 };
-__device__ __forceinline__ StripeBases stripe_bases(const MonoArgs &A, uint32_t stripe) {
+__device__ __forceinline__ StripeBases stripe_bases(const MonoCore &A, uint32_t stripe) {
     return {A.src[0].base + uint64_t(stripe) * A.src_bstride[0], A.src[1].base + uint64_t(stripe) * A.src_bstride[1],
             const_cast<uint8_t *>(A.dst.base) + uint64_t(stripe) * A.dst_bstride};
 }
 
-__device__ __forceinline__ const uint8_t *row_ptr(const MonoArgs &A, const StripeBases &sb, uint32_t r) {
+__device__ __forceinline__ const uint8_t *row_ptr(const MonoCore &A, const StripeBases &sb, uint32_t r) {
     const uint8_t *p = nullptr;
     if (r >= A.src[0].row_begin && r < A.src[0].row_end) p = sb.src0 + uint64_t(r - A.src[0].row_begin) * A.src[0].stride;
     if (A.nsrc > 1 && r >= A.src[1].row_begin && r < A.src[1].row_end)
@@ -679,7 +680,7 @@ __device__ __forceinline__ uint32_t paired_row(uint32_t lane, uint32_t wave, int
 // matrices are read and discarded by the decode's scaling.
 // (2-element packs: the paired words are the 16-bit low and high halves)
 template <int L, int LR, int SPLIT = 0, int E = 4>
-__device__ __forceinline__ void issue_col(const MonoArgs &A, uint32_t chunk, const PackIO &io, const StripeBases &sb,
+__device__ __forceinline__ void issue_col(const MonoCore &A, uint32_t chunk, const PackIO &io, const StripeBases &sb,
                                           uint32_t (&w)[2 << LR], uint32_t lane, uint32_t wave, bool live = true) {
     using S = SeqOf<L, LR, false, SPLIT>;
     const uint32_t base = chunk * (1u << L);
@@ -713,7 +714,7 @@ struct ScaleTabs {
     uint32_t erased;  // bit i: register i's row is not received
 };
 template <int L, int LR, int SPLIT = 0, int E = 4>
-__device__ __forceinline__ void scale_issue(const MonoArgs &A, const uint32_t *rowinfo, ScaleTabs<L, LR, E> &st,
+__device__ __forceinline__ void scale_issue(const MonoCore &A, const uint32_t *rowinfo, ScaleTabs<L, LR, E> &st,
                                             uint32_t lane, uint32_t wave, bool gather = true) {
     constexpr uint32_t PC = Fmt<E>::kPC;
     using S = SeqOf<L, LR, false, SPLIT>;
@@ -768,7 +769,7 @@ __device__ __forceinline__ void finish_col(uint32_t (&w)[2 << LR], const ScaleTa
 }
 
 template <int L, int LR, bool SCALE>
-__device__ __forceinline__ void load_col(const MonoArgs &A, uint32_t chunk, const PackIO &io, const StripeBases &sb,
+__device__ __forceinline__ void load_col(const MonoCore &A, uint32_t chunk, const PackIO &io, const StripeBases &sb,
                                          Col<L, LR> &c, uint32_t lane, uint32_t wave) {
     uint32_t w[2 << LR];
     issue_col<L, LR>(A, chunk, io, sb, w, lane, wave);
@@ -781,7 +782,7 @@ __device__ __forceinline__ void load_col(const MonoArgs &A, uint32_t chunk, cons
 // of the FFT), paired like the loads.  REVEAL (decode): only erased rows,
 // multiplied by exp(65535 - log factor) (rate_high.rs:241-245).
 template <int L, int LR, bool REVEAL, int SPLIT = 0, int E = 4>
-__device__ __forceinline__ void store_col(const MonoArgs &A, const uint32_t *rowinfo, uint32_t chunk,
+__device__ __forceinline__ void store_col(const MonoCore &A, const uint32_t *rowinfo, uint32_t chunk,
                                           const PackIO &io, const StripeBases &sb, Col<L, LR, E> &c, uint32_t lane,
                                           uint32_t wave) {
     using S = SeqOf<L, LR, true, SPLIT>;
@@ -1142,7 +1143,7 @@ __device__ __forceinline__ void vm_wait() {
 // lwv: the thread's lw_fold pair (rows 2t, 2t + 1), loaded by inline asm with
 // NLIVE vector loads issued after it (NSKIP in a wave with `skip`).
 template <int L, int NLIVE, int NSKIP>
-__device__ __forceinline__ void col_eval_poly(const MonoArgs &A, uint32_t ebits, uint32_t rbits, uint32_t lwv,
+__device__ __forceinline__ void col_eval_poly(const MonoCore &A, uint32_t ebits, uint32_t rbits, uint32_t lwv,
                                               bool skip, uint32_t *buf, uint32_t *rinfo) {
     const uint32_t i0 = 2 * threadIdx.x;
     uint32_t x[2];
@@ -1252,9 +1253,13 @@ __device__ __forceinline__ gptr<T> as_global(T *p) {
     return (gptr<T>)p;
 }
 
+// the argument struct of a kernel variant (MonoCore unless the staged decode)
+template <int MODE, bool STAGED>
+using MonoArgT = std::conditional_t<MODE == kMonoDecode && STAGED, MonoArgs, MonoCore>;
+
 template <int L, int LR, int MODE, bool STAGED, bool BATCH, bool SPLIT, int E>
-__device__ __forceinline__ void mono_body(const MonoArgs &K) {
-    MonoArgs A;  // the scalar arguments; the erasure bitmaps stay in K
+__device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
+    MonoCore A;  // the scalar arguments; the erasure bitmaps stay in K
     uint32_t ew[4] = {0, 0, 0, 0}, rw[4] = {0, 0, 0, 0};  // staged decode: the wave's bitmap words
     {
         uint32_t packs = K.packs, ppx = K.packs_per_xcd, nsrc = K.nsrc;
@@ -1347,7 +1352,14 @@ __device__ __forceinline__ void mono_body(const MonoArgs &K) {
         // 0 of phases 1 / 3 from the image when Stage::B0)
         constexpr bool DEC = MODE == kMonoDecode;
         uint32_t *shared = lds + G::plane_words;
-        constexpr uint32_t kSh = DEC ? G::kShared : G::kShared + G::kD;  // shared tables (+ D)
+        // encodes derive phase 3's tables in LDS from phase 1's (+ D tables, below);
+        // RS_MONO_ENC_FETCH3: they fetch them from the FFT image instead
+#ifndef RS_MONO_ENC_FETCH3
+        constexpr bool kDerive3 = !DEC;
+#else
+        constexpr bool kDerive3 = false;
+#endif
+        constexpr uint32_t kSh = kDerive3 ? G::kShared + G::kD : G::kShared;  // shared tables (+ D)
         uint32_t *priv = shared + kSh * G::SW + wave * G::kPriv * G::SW;
         uint32_t *rinfo = lds + G::words;  // decode with fused eval_poly
         constexpr uint32_t PC = G::PC;  // 16-byte pieces per table
@@ -1372,7 +1384,7 @@ __device__ __forceinline__ void mono_body(const MonoArgs &K) {
         // rate_high.rs:213-245), else phase 1's XOR D_b (encodes, Stage::kD)
 #ifndef RS_MONO_NO_REUSE
         const bool same3 = A.ifft_img == A.fft_img;
-        const bool reuse3 = live && (same3 || !DEC);
+        const bool reuse3 = live && (same3 || kDerive3);
 #else
         const bool same3 = A.ifft_img == A.fft_img;
         const bool reuse3 = false;
@@ -1534,7 +1546,7 @@ __device__ __forceinline__ void mono_body(const MonoArgs &K) {
         };
         auto write3 = [&]() {
             if (reuse3) {
-                if constexpr (!DEC) {
+                if constexpr (kDerive3) {
                     if (same3) return;
                     uint4 x[KP3];
                     static_for<0, KP3>([&](auto kc) {
@@ -1660,7 +1672,7 @@ __device__ __forceinline__ void mono_body(const MonoArgs &K) {
 }
 
 template <int L, int LR, int MODE, bool STAGED, bool BATCH, bool SPLIT, int E>
-__global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgs A) {
+__global__ void __launch_bounds__(1 << (L - LR)) k_mono(const MonoArgT<MODE, STAGED> A) {
     mono_body<L, LR, MODE, STAGED, BATCH, SPLIT, E>(A);
 }
 #ifndef RS_MONO_LR10
@@ -1697,7 +1709,8 @@ hipError_t launch_ls(const MonoArgs &A, hipStream_t s) {
         attr_set = true;
     }
     const uint32_t grid = 8u * A.packs_per_xcd;
-    k_mono<L, LR, MODE, STAGED, BATCH, SPLIT, E><<<dim3(grid, BATCH ? A.stripes : 1), 1 << (L - LR), lds, s>>>(A);
+    k_mono<L, LR, MODE, STAGED, BATCH, SPLIT, E>
+        <<<dim3(grid, BATCH ? A.stripes : 1), 1 << (L - LR), lds, s>>>(static_cast<const MonoArgT<MODE, STAGED> &>(A));
     snprintf(launch_name_buf(), kLaunchNameBytes, "k_mono<%d, %d, %d, %s, %s, %s, %d>", L, LR, MODE,
              STAGED ? "true" : "false", BATCH ? "true" : "false", SPLIT ? "true" : "false", E);
     return hipGetLastError();

@@ -83,6 +83,32 @@ def test_encode_device_matches_oracle(torch, rs, rate, N, M, S):
     assert np.array_equal(got, want)
 
 
+# Single-level multi-chunk encodes in both forms (rs_codec.cpp chunk_parallel): chunks one
+# after another in one workgroup (RS_MI355X_CHUNK_PARALLEL=0) and chunks over the grid
+# (=1: HighRate per-chunk IFFT passes + an XOR-fold FFT pass; LowRate one IFFT + FFT per
+# output chunk); the environment is read when a context is created.
+CHUNK_CASES = [("high", 1000, 100, 128), ("low", 100, 1000, 128), ("high", 5000, 300, 256),
+               ("low", 300, 5000, 256), ("high", 129, 1, 64), ("low", 1, 129, 64), ("high", 1000, 64, 8192),
+               ("low", 64, 1000, 8192), ("high", 3000, 200, 130), ("low", 200, 3000, 130)]
+
+
+@pytest.mark.parametrize("forced", ["0", "1"])
+def test_chunk_forms_match_oracle(torch, rs, forced, monkeypatch):
+    monkeypatch.setenv("RS_MI355X_CHUNK_PARALLEL", forced)
+    ctx = rs.Context(0)
+    try:
+        for rate, N, M, S in CHUNK_CASES:
+            orig = O.generate_original(N, S, (N * 13 + M + S) & 0xFF)
+            want = O.encode(rate, orig, M)
+            d_orig = _dev(torch, orig)
+            d_rec = torch.full((M, S), 0xEE, dtype=torch.uint8, device="cuda")
+            rs.encode_device(N, M, S, d_orig, d_rec, rate_=RATE[rate], ctx=ctx)
+            torch.cuda.synchronize()
+            assert np.array_equal(d_rec.cpu().numpy(), want), (forced, rate, N, M, S)
+    finally:
+        ctx.close()
+
+
 DEC_CASES = [
     ("default", 3, 5, 64, 0.5), ("high", 5, 3, 128, 0.5), ("low", 3, 5, 128, 1.0), ("default", 64, 64, 1024, 0.3),
     ("default", 100, 37, 192, 0.2), ("default", 37, 100, 320, 1.0), ("default", 1024, 1024, 1024, 0.01),
