@@ -421,7 +421,12 @@ struct Stage {
     // are phase 1's XOR D_b, one table per phase-3 layer b (twiddles are
     // GF(2)-linear in the global group index, so are the perm tables:
     // D_b = the table of group (t_i ^ t_f) * n / 2^(b+1)), kept after the shared tables
-    static constexpr uint32_t kD = NB3;
+#ifdef RS_MONO_ENC_DERIVE3
+    static constexpr bool kDerive3 = true;
+#else
+    static constexpr bool kDerive3 = false;
+#endif
+    static constexpr uint32_t kD = kDerive3 ? NB3 : 0;
     static constexpr uint32_t words_enc = words + kD * SW;
     static constexpr uint32_t words_dec = words + n;  // + per-row decode info (fused eval_poly)
     // SPLIT decode: + a second column plane (the cross-half step's formal-derivative values)
@@ -1233,7 +1238,11 @@ __device__ __forceinline__ uint32_t priv_layer(uint32_t t) {
 // staged decodes, unless RS_MONO_NO_FLOW)
 constexpr int mono_pk(int mode, bool staged, bool split) {
 #ifndef RS_MONO_NO_FLOW
+#ifndef RS_MONO_ENC_NO_FLOW  // (A/B: the decodes only; encodes measured 8.27 -> 7.90 us with FLOW + fetched phase-3 tables)
+    const bool flow = staged;
+#else
     const bool flow = staged && mode == kMonoDecode;
+#endif
 #else
     const bool flow = false;
 #endif
@@ -1352,13 +1361,10 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
         // 0 of phases 1 / 3 from the image when Stage::B0)
         constexpr bool DEC = MODE == kMonoDecode;
         uint32_t *shared = lds + G::plane_words;
-        // encodes derive phase 3's tables in LDS from phase 1's (+ D tables, below);
-        // RS_MONO_ENC_FETCH3: they fetch them from the FFT image instead
-#ifndef RS_MONO_ENC_FETCH3
-        constexpr bool kDerive3 = !DEC;
-#else
-        constexpr bool kDerive3 = false;
-#endif
+        // encodes fetch phase 3's tables from the FFT image (requested when phase 1
+        // ends); RS_MONO_ENC_DERIVE3: derive them in LDS from phase 1's (+ the D
+        // tables, Stage::kD) -- measured slower with the FLOW plan (profiles/r03j)
+        constexpr bool kDerive3 = !DEC && G::kDerive3;
         constexpr uint32_t kSh = kDerive3 ? G::kShared + G::kD : G::kShared;  // shared tables (+ D)
         uint32_t *priv = shared + kSh * G::SW + wave * G::kPriv * G::SW;
         uint32_t *rinfo = lds + G::words;  // decode with fused eval_poly
