@@ -38,15 +38,18 @@ int main(int argc, char **argv) {
     uint32_t L = 0;
     while ((1u << L) < n) ++L;
     const auto &T = rs::tables();
+    // "...2" in the mode argument: 2-element packs (the codec's decode format)
+    const bool e2 = argc > 3 && std::string(argv[3]).find('2') != std::string::npos;
+    const int tw = e2 ? rs::kPerm2Words : rs::kPermWords;
+    const std::vector<uint32_t> &skew_tabs = e2 ? T.perm2_by_skew : T.perm_by_skew;
     const uint32_t nimg = 65536u / n;
-    const size_t words = size_t(n - 1) * rs::kPermWords;
+    const size_t words = size_t(n - 1) * tw;
     std::vector<uint32_t> h(words * nimg);
     for (uint32_t t = 0; t < nimg; ++t)
         for (uint32_t b = 0; b < L; ++b)
             for (uint32_t g = 0; g < (n >> (b + 1)); ++g) {
                 const uint32_t slot = n - (n >> b) + g, idx = (g << (b + 1)) + (1u << b) + t * n - 1;
-                std::copy_n(&T.perm_by_skew[size_t(idx) * rs::kPermWords], rs::kPermWords,
-                            &h[t * words + size_t(slot) * rs::kPermWords]);
+                std::copy_n(&skew_tabs[size_t(idx) * tw], tw, &h[t * words + size_t(slot) * tw]);
             }
     uint32_t *d_img;
     CK(hipMalloc(&d_img, h.size() * 4));
@@ -56,7 +59,8 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&rec, size_t(n) * S));
     CK(hipMemset(orig, 0x37, size_t(n) * S));
     rs::MonoArgs A;
-    A.packs = S / 8;
+    A.elems = e2 ? 2 : 4;
+    A.packs = e2 ? S / 4 : S / 8;
     A.packs_per_xcd = (A.packs + 7) / 8;
     A.src[0] = rs::RowMap{orig, S, 0, n};
     A.nsrc = 1;
@@ -86,8 +90,9 @@ int main(int argc, char **argv) {
         CK(hipMalloc(&d_lw, n * 2));
         CK(hipMemcpy(d_lw, lw.data(), n * 2, hipMemcpyHostToDevice));
         A.lw_fold = d_lw;
-        CK(hipMalloc(&d_lut, T.perm_by_log.size() * 4));
-        CK(hipMemcpy(d_lut, T.perm_by_log.data(), T.perm_by_log.size() * 4, hipMemcpyHostToDevice));
+        const std::vector<uint32_t> &lut = e2 ? T.perm2_by_log : T.perm_by_log;
+        CK(hipMalloc(&d_lut, lut.size() * 4));
+        CK(hipMemcpy(d_lut, lut.data(), lut.size() * 4, hipMemcpyHostToDevice));
         A.lut = d_lut;
         // "d1": the 1 % pattern (recovery 0..11 and originals 0..n/2-12 received)
         const bool one = argv[3][1] == '1';
@@ -111,7 +116,7 @@ int main(int argc, char **argv) {
     CK(hipEventSynchronize(b));
     float ms;
     CK(hipEventElapsedTime(&ms, a, b));
-    printf("mono %s%s n=%u S=%u: %.2f us/launch (back-to-back)\n", dec ? "decode" : "encode", A.split ? " split" : "", n,
+    printf("mono %s%s%s n=%u S=%u: %.2f us/launch (back-to-back)\n", dec ? "decode" : "encode", A.split ? " split" : "", e2 ? " e2" : "", n,
            S, ms * 1000 / iters);
     {  // floor: an empty kernel with the same grid, block and LDS
         const size_t lds = size_t(rs::Stage<10, 1>::words_dec) * 4;

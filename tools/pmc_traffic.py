@@ -6,7 +6,8 @@ Reads gpurun_out/<tag>/ (rocprofv3 CSV output of tools/gpu_round.sh) and writes
   profiles/<tag>/kernel_stats_<cfg>.csv -- the same for the other configs' benches, when run
   profiles/<tag>/traffic.json           -- per config and kernel: average HBM-side bytes and VALU
                                            wave-instructions per launch
-  profiles/<tag>/sq_<cfg>.csv           -- the raw SQ counter pass of each config
+  (the SQ pass is summarised per kernel into traffic.json: mean of each counter per launch;
+   the raw per-dispatch CSV stays in gpurun_out/)
   profiles/<tag>/bench*.json            -- the bench lines of the same session
 HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md "HBM": FETCH_SIZE and
 WRITE_SIZE (KiB) come from separate --pmc passes; on gfx950 FETCH_SIZE counts
@@ -48,6 +49,11 @@ def summarise(d):
     write = counter_means(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE")
     sq = os.path.join(d, "sq", "run_counter_collection.csv")
     valu = counter_means(sq, "SQ_INSTS_VALU")
+    names = set()
+    if os.path.exists(sq):
+        with open(sq) as f:
+            names = {r["Counter_Name"] for r in csv.DictReader(f)}
+    sq_all = {c: counter_means(sq, c) for c in sorted(names)}
     out = {}
     for k in sorted(set(fetch) | set(valu)):
         if not k.startswith("k_"):
@@ -59,6 +65,7 @@ def summarise(d):
             e.update(fetch_bytes=round(fb), write_bytes=round(wb), hbm_bytes=round(fb + wb), launches=fetch[k][1])
         if k in valu:
             e.update(valu_insts=round(valu[k][0]), valu_launches=valu[k][1])
+            e["sq"] = {c: round(m[k][0]) for c, m in sq_all.items() if k in m}
         out[k] = e
     return out
 
@@ -74,9 +81,6 @@ def main(tag):
     pmc = os.path.join(src, "pmc")
     for cfg in sorted(os.listdir(pmc)) if os.path.isdir(pmc) else []:
         configs[cfg] = summarise(os.path.join(pmc, cfg))
-        sq = os.path.join(pmc, cfg, "sq", "run_counter_collection.csv")
-        if os.path.exists(sq):
-            shutil.copy(sq, os.path.join(dst, f"sq_{cfg}.csv"))
     kt = os.path.join(src, "kt")
     for cfg in sorted(os.listdir(kt)) if os.path.isdir(kt) else []:
         f = os.path.join(kt, cfg, "run_kernel_stats.csv")
