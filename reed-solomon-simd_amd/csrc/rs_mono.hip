@@ -33,7 +33,7 @@ namespace rs {
 namespace {
 
 #ifdef RS_MONO_STAMPS  // tools/mono_probe.hip: per-workgroup timestamps
-__device__ uint64_t g_mono_stamps[4096][16];
+__device__ uint64_t g_mono_stamps[4096][24];
 #ifdef RS_MONO_STAMP_WAIT  // each stamp first waits for the wave's outstanding memory ops
 #define RS_MSTAMP_WAIT() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
 #else  // the time the wave's instruction stream reaches the stamp
@@ -710,14 +710,63 @@ __device__ __forceinline__ void issue_col(const MonoCore &A, uint32_t chunk, con
     });
 }
 
+// Per-row multiply tables gathered by a quad of lanes (2-element format).  A
+// gathered table is one 64-byte line per row; a lane fetching its own row's 4
+// pieces touches up to 64 lines per wave instruction, and those gathers bound
+// the decode's prologue (the texture path resolves about one line per clock).
+// Instead lane p of a quad loads piece p of each of the quad's 4 tables (4
+// lanes, one line: 16 lines per instruction), and the multiply is split the
+// same way: piece p holds the lookups of 2-bit field p (gf_muladd2's d_p and
+// c_p), so lane p forms field p's partial product for all 4 rows and a
+// reduce-scatter over the quad XORs them into each row's product.
+template <int K>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {  // lane 4j + K's value, to the whole quad
+    return __builtin_amdgcn_update_dpp(0, int(v), K * 0x55, 0xF, 0xF, false);
+}
+// t[4k .. 4k + 3] = piece (lane & 3) of table lut[lg of quad lane k]
+__device__ __forceinline__ void quad_gather2(const uint32_t *lut, uint32_t lg, uint32_t lane, uint32_t (&t)[16]) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(lut) + (lane & 3u);
+    static_for<0, 4>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const uint4 v = q[quad_bcast<k>(lg) * 4u];
+        t[4 * k] = v.x, t[4 * k + 1] = v.y, t[4 * k + 2] = v.z, t[4 * k + 3] = v.w;
+    });
+}
+// x * m of this lane's row, t from quad_gather2 (all 4 lanes of the quad take part)
+__device__ __forceinline__ uint32_t quad_mul2(uint32_t x, const uint32_t (&t)[16], uint32_t lane) {
+    constexpr uint32_t M = 0x03030303u, C = 0x04040000u;
+    auto sel = [](uint32_t v) { return __builtin_amdgcn_bitop3_b32(v, M, C, 0xEA); };
+    const uint32_t sh = 2u * (lane & 3u);
+    uint32_t part[4];
+    static_for<0, 4>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const uint32_t xk = quad_bcast<k>(x);
+        const uint32_t xr = __builtin_amdgcn_alignbit(xk, xk, 16);
+        const uint64_t s = ((uint64_t(xr) << 32) | xk) >> sh;
+        part[k] = __builtin_amdgcn_perm(t[4 * k + 1], t[4 * k], sel(uint32_t(s))) ^
+                  __builtin_amdgcn_perm(t[4 * k + 3], t[4 * k + 2], sel(uint32_t(s >> 32)));
+    });
+    // reduce-scatter: lane p ends with the XOR over the quad of part[p]
+    const bool b1 = lane & 2u, b0 = lane & 1u;
+    const uint32_t k0 = (b1 ? part[2] : part[0]) ^ xor_lane<1>(b1 ? part[0] : part[2]);
+    const uint32_t k1 = (b1 ? part[3] : part[1]) ^ xor_lane<1>(b1 ? part[1] : part[3]);
+    return (b0 ? k1 : k0) ^ xor_lane<0>(b0 ? k0 : k1);
+}
+
 // Decode scaling (rate_high.rs:213-231): received rows are multiplied by
 // exp(log factor), erased rows become zero; rowinfo is indexed by work row.
-// scale_issue requests the multiply tables, finish_col applies them.
+// scale_issue requests the multiply tables, finish_col applies them
+// (2-element packs: quad-gathered, quad_gather2 / quad_mul2).
 template <int L, int LR, int E = 4>
 struct ScaleTabs {
     uint32_t t[1 << LR][Fmt<E>::kTW];
     uint32_t erased;  // bit i: register i's row is not received
 };
+#ifndef RS_MONO_NO_QUAD_GATHER  // (A/B: per-lane gathers of whole tables)
+constexpr bool kQuadGather = true;
+#else
+constexpr bool kQuadGather = false;
+#endif
 template <int L, int LR, int SPLIT = 0, int E = 4>
 __device__ __forceinline__ void scale_issue(const MonoCore &A, const uint32_t *rowinfo, ScaleTabs<L, LR, E> &st,
                                             uint32_t lane, uint32_t wave, bool gather = true) {
@@ -738,7 +787,9 @@ __device__ __forceinline__ void scale_issue(const MonoCore &A, const uint32_t *r
         // are unconditional and the waits for the table staging loads issued
         // before them stay exact (see issue_col)
         if (f & 0x10000u) lg = 0;
-        if (gather) {  // (wave-uniform: a wave with no received row skips them)
+        if constexpr (E == 2 && kQuadGather) {
+            if (gather) quad_gather2(A.lut, lg, lane, st.t[i]);
+        } else if (gather) {  // (wave-uniform: a wave with no received row skips them)
             const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + lg * PC;
 #pragma unroll
             for (int v = 0; v < int(PC); ++v) {
@@ -759,7 +810,8 @@ __device__ __forceinline__ void finish_col(uint32_t (&w)[2 << LR], const ScaleTa
         if constexpr (E == 2) {
             c.lo[i] = w[2 * i] | (w[2 * i + 1] << 16);
             if constexpr (SCALE) {
-                gf_mul2(c.lo[i], st->t[i]);
+                if constexpr (kQuadGather) c.lo[i] = quad_mul2(c.lo[i], st->t[i], lane);
+                else gf_mul2(c.lo[i], st->t[i]);
                 if ((st->erased >> i) & 1u) c.lo[i] = 0;
             }
         } else {
@@ -783,13 +835,41 @@ __device__ __forceinline__ void load_col(const MonoCore &A, uint32_t chunk, cons
     finish_col<L, LR, SCALE, 4>(w, &st, c, lane);
 }
 
+// Reveal (decode, rate_high.rs:241-245): the multiply tables exp(65535 - log
+// factor) of the lane's rows at the end of the FFT, for erased rows inside
+// A.dst (the others read one shared dummy table, log 0: no extra cache lines).
+// 2-element packs gather them ahead (reveal_issue, quad-gathered, before the
+// FFT's last in-wave phase), so store_col does not wait for them.
+template <int LR>
+struct RevealTabs {
+    uint32_t t[1 << LR][16];
+};
+template <typename S, int I, int LR>
+__device__ __forceinline__ uint32_t reveal_log(const MonoCore &A, const uint32_t *rowinfo, uint32_t r) {
+    const uint32_t f = rowinfo[r];
+    const bool need = (f & 0x10000u) && r >= A.dst.row_begin && r < A.dst.row_end;
+    return need ? 65535u - (f & 0xFFFFu) : 0u;
+}
+template <int L, int LR, int SPLIT = 0>
+__device__ __forceinline__ void reveal_issue(const MonoCore &A, const uint32_t *rowinfo, RevealTabs<LR> &rt,
+                                             uint32_t lane, uint32_t wave) {
+    using S = SeqOf<L, LR, true, SPLIT>;
+    constexpr int I = S::v.count;
+    const uint32_t a = lane_rows<S, I>(lane, wave);
+    static_for<0, (1 << LR)>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        quad_gather2(A.lut, reveal_log<S, I, LR>(A, rowinfo, a | reg_rows<S, I, LR>(i)), lane, rt.t[i]);
+    });
+}
+
 // Store transform rows `chunk * n + row` that fall in A.dst (placement: end
 // of the FFT), paired like the loads.  REVEAL (decode): only erased rows,
-// multiplied by exp(65535 - log factor) (rate_high.rs:241-245).
+// multiplied by exp(65535 - log factor) (rate_high.rs:241-245); rt: tables
+// from reveal_issue (2-element packs), else gathered here.
 template <int L, int LR, bool REVEAL, int SPLIT = 0, int E = 4>
 __device__ __forceinline__ void store_col(const MonoCore &A, const uint32_t *rowinfo, uint32_t chunk,
                                           const PackIO &io, const StripeBases &sb, Col<L, LR, E> &c, uint32_t lane,
-                                          uint32_t wave) {
+                                          uint32_t wave, const RevealTabs<LR> *rt = nullptr) {
     using S = SeqOf<L, LR, true, SPLIT>;
     constexpr uint32_t PC = Fmt<E>::kPC;
     constexpr int I = S::v.count;
@@ -799,12 +879,14 @@ __device__ __forceinline__ void store_col(const MonoCore &A, const uint32_t *row
         const uint32_t a = lane_rows<S, I>(lane, wave) + base;
         static_for<0, R>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
+            if constexpr (E == 2) {
+                if (rt) {
+                    c.lo[i] = quad_mul2(c.lo[i], rt->t[i], lane);
+                    return;
+                }
+            }
             const uint32_t r = a | reg_rows<S, I, LR>(i);
-            const uint32_t f = rowinfo[r];
-            // only erased rows inside A.dst are revealed; the others read one
-            // shared dummy table (log 0), so their gathers cost no cache lines
-            const bool need = (f & 0x10000u) && r >= A.dst.row_begin && r < A.dst.row_end;
-            const uint32_t lg = need ? 65535u - (f & 0xFFFFu) : 0u;
+            const uint32_t lg = reveal_log<S, I, LR>(A, rowinfo, r);
             uint32_t t[Fmt<E>::kTW];
             const uint4 *q = reinterpret_cast<const uint4 *>(A.lut) + lg * PC;
 #pragma unroll
@@ -1083,7 +1165,15 @@ __device__ __forceinline__ uint32_t walsh_fold(uint32_t x) {
     return (x & 0xFFFFu) + (x >> 16);  // < 2^16, same residue mod 65535
 }
 
+// rounds of LDS exchanges of one col_walsh (two wave-bit layers per round)
 template <int L>
+constexpr int kWalshRounds = ((L > 7 ? L - 7 : 0) + 1) / 2;
+// G0: index of the transform's first round among the decode's consecutive rounds.
+// Round g uses buffer (g even: buf + 2^L words, g odd: buf); the two transforms
+// have the same even number of rounds in all, so the last one reads buf and
+// every buffer is rewritten only after a barrier that follows its last reads
+// (no barrier between the transforms; see col_eval_poly)
+template <int L, int G0 = 0, int ST = -1>
 __device__ __forceinline__ void col_walsh(uint32_t (&x)[2], uint32_t *buf) {
     const uint32_t t = threadIdx.x, lane = t & 63u;
     {
@@ -1102,6 +1192,7 @@ __device__ __forceinline__ void col_walsh(uint32_t (&x)[2], uint32_t *buf) {
             x[q] = y + (x[q] ^ m) + c;
         });
     });
+    if constexpr (ST >= 0) RS_MSTAMP(ST);
     // wave bits: two layers per LDS round (each thread reads its group's 3
     // partners), ping-pong buffers so one barrier per round suffices
     static_for<0, ((L > 7 ? L - 7 : 0) + 1) / 2>([&](auto rc) {
@@ -1111,7 +1202,7 @@ __device__ __forceinline__ void col_walsh(uint32_t (&x)[2], uint32_t *buf) {
         constexpr uint32_t h1 = 1u << (j - 1), h2 = two ? 1u << j : 0u;  // thread bits
         // a thread's two values as one 8-byte word: ds_write_b64 / ds_read_b64 of
         // consecutive threads are conflict-free (stride-2 32-bit accesses were 2-way)
-        uint2 *b = reinterpret_cast<uint2 *>(buf + ((rnd & 1) << L));
+        uint2 *b = reinterpret_cast<uint2 *>(buf + ((((G0 + rnd) & 1) ^ 1) << L));
         b[t] = uint2{x[0], x[1]};
         __syncthreads();
         const uint32_t m1 = (t & h1) ? ~0u : 0u, c1 = m1 & kWalshM1<j>;
@@ -1137,7 +1228,7 @@ __device__ __forceinline__ void col_walsh(uint32_t (&x)[2], uint32_t *buf) {
 
 // rinfo[r] = log factor | (received ? 0 : 0x10000) for the 2^L work rows.
 // ebits / rbits: this thread's erased / received bits (bits 0, 1 = rows 2t,
-// 2t+1); lw: lw_fold of those rows.  Ends with a barrier.
+// 2t+1); lw: lw_fold of those rows.  No barrier at the end (see the rinfo store).
 // s_waitcnt vmcnt(N) (a load the compiler does not track: see mono_body)
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -1158,7 +1249,7 @@ __device__ __forceinline__ void col_eval_poly(const MonoCore &A, uint32_t ebits,
         // high rate: v = e;  low rate: v = e - 1 on [0, end), 0 beyond  (rate_low.rs:196)
         x[k] = A.low_rate ? (i < A.end ? (e ? 0u : 65534u) : 0u) : e;
     });
-    col_walsh<L>(x, buf);
+    col_walsh<L, 0, 19>(x, buf);
     RS_MSTAMP(14);
     if (skip) vm_wait<NSKIP>();
     else vm_wait<NLIVE>();
@@ -1171,11 +1262,15 @@ __device__ __forceinline__ void col_eval_poly(const MonoCore &A, uint32_t ebits,
         if (A.low_rate && i0 + k == 0) f = ev_add(f, A.lw0);
         x[k] = f;
     });
-    if constexpr (L > 7) __syncthreads();  // the first transform's last LDS reads are done
-    col_walsh<L>(x, buf);
+    col_walsh<L, kWalshRounds<L>, 20>(x, buf);
+    // rinfo of rows 2t, 2t + 1: read next (scale_issue) by the same wave -- the
+    // IFFT's first placement gives wave w rows [2^IW w, 2^IW (w + 1)) like this
+    // one -- so no barrier: the LDS executes a wave's accesses in order.  The
+    // LDS written next (table staging over the second exchange buffer) was last
+    // read before the last round's barrier
     reinterpret_cast<uint2 *>(rinfo)[threadIdx.x] =
         uint2{x[0] | ((rbits & 1u) ? 0u : 0x10000u), x[1] | ((rbits & 2u) ? 0u : 0x10000u)};
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 // ---------------------------------------------------------------------------
@@ -1474,23 +1569,27 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
 #define RS_MONO_DEC_ORDER 1
 #endif
         constexpr int kOrder = RS_MONO_DEC_ORDER;
-        constexpr bool kShFirst = kOrder != 2, kPrivFirst = kOrder == 1;
+        // 4: the shared tables only, eval_poly, then rows, gathers, phase-1 tables
+        constexpr bool kShFirst = kOrder != 2, kPrivFirst = kOrder == 1, kRowsFirst = kOrder != 4;
         if constexpr (!DEC) {
             issue_rows();
             issue_priv();
             issue_shared();
         } else {
             if constexpr (kShFirst) issue_shared();
+            RS_MSTAMP(16);
             if (!skip) {
-                issue_rows();
+                if constexpr (kRowsFirst) issue_rows();
+                RS_MSTAMP(17);
                 if constexpr (kPrivFirst) issue_priv();
             }
+            RS_MSTAMP(18);
         }
         const uint32_t *ri = A.rowinfo;
         if constexpr (DEC) {
             // vector loads issued after lw_fold's (see above), per branch
             constexpr int kAfterSkip = kShFirst ? kShLoads : 0;
-            constexpr int kAfterLive = kAfterSkip + kRowLoads + (kPrivFirst ? kPrivLoads : 0);
+            constexpr int kAfterLive = kAfterSkip + (kRowsFirst ? kRowLoads : 0) + (kPrivFirst ? kPrivLoads : 0);
 #ifndef RS_MONO_SKIP_EVAL  // tools/mono_probe.hip ablation
             col_eval_poly<L, kAfterLive, kAfterSkip>(A, ebits, rbits, lwv, skip, plane, rinfo);
 #else
@@ -1506,6 +1605,8 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
         ScaleTabs<L, LR, E> st;
         // (decodes) the scale gathers go out as soon as eval_poly is done
         if constexpr (DEC) {
+            if constexpr (!kRowsFirst)
+                if (!skip) issue_rows();
             scale_issue<L, LR, PK, E>(A, ri, st, lane, wave, !skip);
             if constexpr (!kShFirst) issue_shared();
             if constexpr (!kPrivFirst)
@@ -1594,6 +1695,17 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                     if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at0(q)] = v4[kc];
                 });
         };
+        // 2-element decodes: the reveal tables are requested just before the FFT's
+        // last remap (with phase 3's table writes), so they land while phase 3 runs
+        constexpr bool kPreReveal = DEC && E == 2 && kQuadGather;
+        RevealTabs<LR> rt;
+        auto pre3 = [&](bool alive) {
+            return [&, alive]() {
+                write3();
+                if constexpr (kPreReveal)
+                    if (alive) reveal_issue<L, LR, PK>(A, ri, rt, lane, wave);
+            };
+        };
         if constexpr (SPLIT) {
             // the wave's half: the highest wave bit in both placements
             constexpr uint32_t kHalfWords = (G::n / 2) / 32;
@@ -1615,8 +1727,8 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             RS_MSTAMP(6);
             issue4(alive);
             // FFT below the top layer: only the half that holds restored rows
-            run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, PK>(ts, c, plane, lane, wave, write3, alive,
-                                                                              out, write4);
+            run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, PK>(ts, c, plane, lane, wave, pre3(alive),
+                                                                              alive, out, write4);
             if (!alive) return;
         } else if constexpr (G::WB > 0) {
             run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 1 : -1, PK>(ts, c, plane, lane, wave, issue3, true, live,
@@ -1627,8 +1739,8 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             const bool alive = !DEC || wave_stores<L, LR, PK>(A, wave);
             issue4(alive);  // (waves that stop early all read one table: no branch around the loads)
             if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
-            run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, PK>(ts, c, plane, lane, wave, write3, alive, true,
-                                                                        write4);
+            run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, PK>(ts, c, plane, lane, wave, pre3(alive), alive,
+                                                                        true, write4);
             if (!alive) return;
         } else {
             static_assert(!G::B0, "one-segment plans keep every table in the region");
@@ -1639,7 +1751,7 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             run_seq<L, LR, true, RS_MONO_LDS_PF, -1, PK>(ts, c, plane, lane, wave, NoHook{});
         }
         RS_MSTAMP(10);
-        store_col<L, LR, DEC, PK>(A, ri, 0, io, sb, c, lane, wave);
+        store_col<L, LR, DEC, PK>(A, ri, 0, io, sb, c, lane, wave, kPreReveal && G::WB > 0 ? &rt : nullptr);
         RS_MSTAMP(11);
     } else if constexpr (MODE == kMonoEncodeHigh) {
         // rate_high.rs:44-87: recovery = FFT_0(XOR_c IFFT_{c n + n}(chunk c))

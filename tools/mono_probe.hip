@@ -136,7 +136,7 @@ int main(int argc, char **argv) {
     go();
     CK(hipDeviceSynchronize());
     const uint32_t wgs = 8 * A.packs_per_xcd;
-    std::vector<uint64_t> st(4096 * 16);
+    std::vector<uint64_t> st(4096 * 24);
     CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(rs::g_mono_stamps), st.size() * 8));
     // s_memrealtime is per XCD: entry spread within each XCD's workgroups
     // (b % 8), stages as per-workgroup deltas from the workgroup's wave-0 entry
@@ -144,18 +144,19 @@ int main(int argc, char **argv) {
         double sp = 0;
         for (uint32_t x = 0; x < 8; ++x) {
             uint64_t lo = ~0ull, hi = 0;
-            for (uint32_t w = x; w < wgs; w += 8) lo = std::min(lo, st[w * 16 + 12]), hi = std::max(hi, st[w * 16 + 12]);
+            for (uint32_t w = x; w < wgs; w += 8) lo = std::min(lo, st[w * 24 + 12]), hi = std::max(hi, st[w * 24 + 12]);
             sp = std::max(sp, (hi - lo) * 0.01);
         }
         printf("entry spread within an XCD (worst XCD): %.2f us\n", sp);
     }
-    const char *names[16] = {"start", "loaded", "eval done", "ifft A done", "remap1 done", "ifft B done", "split done", "entry",
+    const char *names[24] = {"start", "loaded", "eval done", "ifft A done", "remap1 done", "ifft B done", "split done", "entry",
                              "fft B done", "remap2 done", "fft C done", "stored", "entry wave0", "loads issued",
-                             "walsh1 done", "lw landed"};
-    const int order[] = {12, 7, 0, 14, 15, 2, 13, 1, 3, 4, 5, 6, 8, 9, 10, 11};
+                             "walsh1 done", "lw landed", "shared issued", "rows issued", "priv issued", "walsh1 in-wave",
+                             "walsh2 in-wave", "", "", ""};
+    const int order[] = {12, 7, 0, 16, 17, 18, 19, 14, 15, 20, 2, 13, 1, 3, 4, 5, 6, 8, 9, 10, 11};
     for (int i : order) {
         std::vector<double> v;
-        for (uint32_t w = 0; w < wgs; ++w) v.push_back((double(st[w * 16 + i]) - double(st[w * 16 + 12])) * 0.01);
+        for (uint32_t w = 0; w < wgs; ++w) v.push_back((double(st[w * 24 + i]) - double(st[w * 24 + 12])) * 0.01);
         std::sort(v.begin(), v.end());
         printf("%-12s min %6.2f  med %6.2f  max %6.2f us\n", names[i], v.front(), v[v.size() / 2], v.back());
     }
