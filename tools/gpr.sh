@@ -6,7 +6,7 @@ LOG=$1; TO=$2; CMD=$3
 for i in 1 2 3 4 5 6 7 8; do
   /usr/local/graft/bin/gpurun --timeout "$TO" -- "$CMD" > "$LOG" 2>&1
   rc=$?
-  if [ $rc -eq 3 ] || grep -q "status=transient" "$LOG"; then sleep 60; continue; fi
+  if [ $rc -eq 3 ] || grep -q -E "status=transient|backing off" "$LOG"; then sleep 75; continue; fi
   exit $rc
 done
 exit $rc
