@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rs_device.hpp"
+#include "rs_gf.hpp"
 
 namespace rs {
 namespace {
@@ -102,6 +103,128 @@ __global__ void __launch_bounds__(1024) k_eval_poly(const EvalArgs A) {
     RS_ESTAMP(5);
 }
 
+// 2^11 and 2^12 points (pass-kernel decodes of 2048 / 4096 work rows): one
+// workgroup of 1024 threads, thread t holding rows t*V .. t*V + V - 1
+// (V = 2^(u - 10)), the transform as in the column kernel's fused eval_poly
+// (rs_mono.hip col_walsh): log2(V) layers in registers, 6 across lanes by DPP /
+// v_permlane*_swap, the 4 wave bits as two LDS rounds of two layers, lazy
+// reduction mod 65535 (values below B_k after k layers, folded at the end).
+// It replaces 22 one-layer barriers (2^11: 8.2 -> 3.2..5.0 us per launch) or
+// three launches (2^12: 10.0 -> 5.0 us; tools/eval_probe.hip, profiles/r03b).
+template <int J>
+__device__ __forceinline__ uint32_t ev_lane_xor(uint32_t v, uint32_t lane) {  // value of lane ^ 2^J
+    if constexpr (J == 4) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16u) ? r[0] : r[1];
+    } else if constexpr (J == 5) {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32u) ? r[0] : r[1];
+    } else if constexpr (J == 0) {
+        return __builtin_amdgcn_update_dpp(0, int(v), 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+    } else if constexpr (J == 1) {
+        return __builtin_amdgcn_update_dpp(0, int(v), 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+    } else if constexpr (J == 2) {  // row_half_mirror of quad_perm 3,2,1,0
+        return __builtin_amdgcn_update_dpp(0, __builtin_amdgcn_update_dpp(0, int(v), 0x1B, 0xF, 0xF, false), 0x141,
+                                           0xF, 0xF, false);
+    } else {
+        return __builtin_amdgcn_update_dpp(0, int(v), 0x128, 0xF, 0xF, false);  // row_ror:8
+    }
+}
+constexpr uint64_t ev_bound(int k) {  // B_k: values stay below it after k lazy layers
+    uint64_t b = 65536u;
+    for (int i = 0; i < k; ++i) b = 2 * b + 65535u;
+    return b;
+}
+template <int K>  // M_K + 1, M_K the least multiple of 65535 >= B_K
+constexpr uint32_t kEvM1 = uint32_t((ev_bound(K) + 65534u) / 65535u * 65535u) + 1u;
+static_assert(ev_bound(13) < (1ull << 32), "lazy Walsh-Hadamard bound at 2^13 points");
+__device__ __forceinline__ uint32_t ev_fold(uint32_t x) {
+    x = (x & 0xFFFFu) + (x >> 16);
+    return (x & 0xFFFFu) + (x >> 16);
+}
+
+// One 2^(LV + 10)-point transform; G0: index of its first LDS round (rounds
+// alternate the two buffers across both transforms, so no barrier between them)
+template <int LV, int G0>
+__device__ __forceinline__ void walsh_fast(uint32_t (&x)[1 << LV], uint32_t *buf) {
+    constexpr int V = 1 << LV, L = LV + 10;
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    static_for<0, LV>([&](auto kc) {  // register bits
+        constexpr int k = decltype(kc)::value;
+        static_for<0, V>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            if constexpr (!(v & (1 << k))) {
+                const uint32_t a = x[v], b = x[v | (1 << k)];
+                x[v] = a + b;
+                x[v | (1 << k)] = a + ~b + kEvM1<k>;
+            }
+        });
+    });
+    static_for<0, 6>([&](auto jc) {  // lane bits
+        constexpr int J = decltype(jc)::value;
+        const uint32_t m = (lane & (1u << J)) ? ~0u : 0u, c = m & kEvM1<LV + J>;
+        static_for<0, V>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            x[v] = ev_lane_xor<J>(x[v], lane) + (x[v] ^ m) + c;
+        });
+    });
+    static_for<0, 2>([&](auto rc) {  // wave bits: thread bits 6 + 2 rnd, 7 + 2 rnd
+        constexpr int rnd = decltype(rc)::value;
+        constexpr int j = LV + 6 + 2 * rnd;  // layers j, j + 1
+        constexpr uint32_t h1 = 64u << (2 * rnd), h2 = h1 << 1;
+        uint32_t *b = buf + ((((G0 + rnd) & 1) ^ 1) << L);
+        static_for<0, V>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            b[t * V + v] = x[v];
+        });
+        __syncthreads();
+        const uint32_t m1 = (t & h1) ? ~0u : 0u, c1 = m1 & kEvM1<j>;
+        const uint32_t m2 = (t & h2) ? ~0u : 0u, c2 = m2 & kEvM1<j + 1>;
+        const uint32_t g0 = t & ~(h1 | h2);
+        static_for<0, V>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            const uint32_t v00 = b[g0 * V + v], v01 = b[(g0 | h1) * V + v];
+            const uint32_t v10 = b[(g0 | h2) * V + v], v11 = b[(g0 | h1 | h2) * V + v];
+            const uint32_t lo = v00 + (v01 ^ m1) + c1, hi = v10 + (v11 ^ m1) + c1;
+            x[v] = lo + (hi ^ m2) + c2;
+        });
+    });
+    static_for<0, V>([&](auto vc) { x[decltype(vc)::value] = ev_fold(x[decltype(vc)::value]); });
+}
+
+template <int LV>
+__global__ void __launch_bounds__(1024) k_eval_fast(const EvalArgs A) {
+    constexpr int V = 1 << LV;
+    extern __shared__ __attribute__((aligned(16))) uint32_t ebuf[];  // 2 x 2^(LV + 10) words
+    const uint32_t r0 = threadIdx.x * V;
+    uint32_t lw[V], x[V];
+    static_for<0, V>([&](auto vc) { lw[decltype(vc)::value] = A.lw_fold[r0 + decltype(vc)::value]; });
+    // V consecutive rows lie in one bitmap word (inline bitmaps: 2^u <= kEvalInlineRows)
+    const uint32_t eb = A.erased[r0 >> 5] >> (r0 & 31u), rb = A.received[r0 >> 5] >> (r0 & 31u);
+    static_for<0, V>([&](auto vc) {
+        constexpr int v = decltype(vc)::value;
+        const uint32_t e = (eb >> v) & 1u, i = r0 + v;
+        // high rate: v = e;  low rate: v = e - 1 on [0, end), 0 beyond  (rate_low.rs:196)
+        x[v] = A.low_rate ? (i < A.end ? (e ? 0u : 65534u) : 0u) : e;
+    });
+    walsh_fast<LV, 0>(x, ebuf);
+    static_for<0, V>([&](auto vc) {
+        constexpr int v = decltype(vc)::value;
+        const uint32_t p = x[v] * lw[v];
+        uint32_t f = add_mod(p & 0xFFFFu, p >> 16);
+        if (A.low_rate && r0 + v == 0) f = add_mod(f, A.lw0);
+        x[v] = f;
+    });
+    walsh_fast<LV, 2>(x, ebuf);
+    static_for<0, V>([&](auto vc) {
+        constexpr int v = decltype(vc)::value;
+        A.rowinfo[r0 + v] = x[v] | (((rb >> v) & 1u) ? 0u : 0x10000u);
+    });
+}
+#ifndef RS_EVAL_FAST_MIN_U  // (A/B: 14 = off)
+#define RS_EVAL_FAST_MIN_U 11
+#endif
+
 // Large transforms (2^u > kEvalSingleRows) spread over many workgroups: the
 // two FWHT_u split into their low bits [0, K1) and high bits [K1, u), four
 // launches, one workgroup per set of 2^K values that differ only in those
@@ -170,6 +293,25 @@ __global__ void __launch_bounds__(512) k_walsh_part(const EvalArgs A, uint32_t a
 
 hipError_t launch_eval_poly(const EvalArgs &A, hipStream_t s) {
     const uint32_t n = 1u << A.u;
+    // (2^13 points measured no faster than the three launches: 10.8 vs 10.6 us)
+    if (A.u >= RS_EVAL_FAST_MIN_U && A.u <= 12) {
+        static_assert((1u << 13) <= kEvalInlineRows, "k_eval_fast reads the inline bitmaps");
+        const size_t lds = size_t(8) * n;  // two exchange buffers of 2^u words
+        static bool fast_attr = false;  // benign race: idempotent attribute calls
+        if (!fast_attr) {
+            for (const void *k : {reinterpret_cast<const void *>(&k_eval_fast<1>),
+                                  reinterpret_cast<const void *>(&k_eval_fast<2>),
+                                  reinterpret_cast<const void *>(&k_eval_fast<3>)}) {
+                hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+                if (e != hipSuccess) return e;
+            }
+            fast_attr = true;
+        }
+        if (A.u == 11) k_eval_fast<1><<<1, 1024, lds, s>>>(A);
+        else if (A.u == 12) k_eval_fast<2><<<1, 1024, lds, s>>>(A);
+        else k_eval_fast<3><<<1, 1024, lds, s>>>(A);
+        return hipGetLastError();
+    }
     if (n > kEvalSingleRows) {
         const uint32_t K1 = A.u / 2, K2 = A.u - K1;
         const auto go = [&](auto kern, uint32_t a, uint32_t K) {
