@@ -197,6 +197,10 @@ def make_timer(world, dev):
         """GPU time of `steps` calls from events on the launch stream (separate, untimed pass)."""
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
+        # one untimed call first: ev0 then completes behind work already on the GPU, not
+        # ahead of the host's first launch into an idle queue (that gap read as ≈+1 µs per
+        # step at 20 steps and made this launch-scope duration exceed the wall time per step)
+        fn()
         ev0.record(stream)
         for _ in range(steps):
             fn()
