@@ -69,6 +69,7 @@ def parse():
     p.add_argument("--no-copy", action="store_true", help="skip the 1 GiB device-copy context measurement")
     p.add_argument("--no-decode", action="store_true")
     p.add_argument("--no-host", action="store_true", help="skip the host-memory end-to-end measurement")
+    p.add_argument("--no-object", action="store_true", help="skip the object-API (encoder/decoder) measurement")
     p.add_argument("--profile-steps", type=int, default=50)
     p.add_argument("--batch", type=int, default=64, help="stripes per call of the batched measurement (1 = skip)")
     p.add_argument("--plumbing", action="store_true",
@@ -386,6 +387,12 @@ def stripe_bench(args, rs, ctx, config, world, rank, dev):
                     "decode_1pct_GiBps": round(world * step_bytes / ddt / 2**30, 3), "slices": best[0],
                     "note": "pinned host buffers, hipMemcpy2DAsync in + kernels + out, column slices over 3 streams"}
 
+    # ---- the drop-in object API (rank 0): ReedSolomonEncoder / Decoder calls as
+    # the reference's benchmark makes them, through the C ABI in native code ----
+    object_api = None
+    if rank == 0 and not args.no_object:
+        object_api = object_api_bench(N, M, S, max(20, args.steps // 4), 5)
+
     copy_ref = None if args.no_copy else device_copy(dev)
 
     # ---- CPU baseline (rank 0, N = 1 only) ----------------------------------
@@ -406,11 +413,33 @@ def stripe_bench(args, rs, ctx, config, world, rank, dev):
             "decode_GiBps": decode,
             "batched": batched,
             "host_e2e": host_e2e,
+            "object_api": object_api,
             "roofline": roofline,
             "device_copy": copy_ref,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
+
+
+def object_api_bench(N, M, S, iters, warmup):
+    """The object API in the reference benchmark's scope (benches/benchmarks.rs:97-139):
+    N x rs_encoder_add_original_shard + rs_encoder_encode, and the decoder at 1 % / 100 %
+    loss, host shards in and out, timed by tools/object_bench.cpp (built by build()) in a
+    child process -- what a Rust caller of the INTEGRATION.md shim pays per call."""
+    exe = os.path.join(ROOT, "reed-solomon-simd_amd", "lib", "rs_object_bench")
+    if not os.path.exists(exe):
+        return {"error": "rs_object_bench not built (run __graft_entry__.build())"}
+    try:
+        out = subprocess.run([exe, str(N), str(M), str(S), str(iters), str(warmup)], capture_output=True,
+                             text=True, timeout=300)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    if out.returncode != 0:
+        return {"error": (out.stderr or out.stdout).strip()[-300:]}
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    r["note"] = ("C ABI from native code: add shards (host, pinned staging) + encode/decode; one stream, "
+                 "received rows in, recovery/restored rows out (PCIe included)")
+    return r
 
 
 def device_copy(dev):

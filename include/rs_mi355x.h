@@ -40,9 +40,14 @@
  * then pass a new stream that reuses its handle.  A context keeps the scratch
  * of at most RS_MAX_STREAM_WORKSPACES streams (device buffers sized to the
  * largest call made on each, plus pinned staging); a call on a further stream
- * first synchronizes the device and frees the least recently used stream's
- * scratch.  rs_release_stream_scratch frees one stream's scratch at once (call
- * it before destroying a stream the context has seen).  Every entry point runs on
+ * takes over the least recently used stream's scratch (buffers kept, no free)
+ * after waiting for that stream's last call -- by an event recorded at the end
+ * of each call once 8 or more streams are in use, else by synchronizing the
+ * device.  rs_release_stream_scratch frees one stream's scratch at once (call
+ * it before destroying a stream the context has seen).  Single-level HighRate
+ * encodes with several chunks and few packs spread the chunks over the grid,
+ * with a work buffer of about the input's size, only up to 256 MiB of it; larger
+ * ones run the chunks in sequence without one.  Every entry point runs on
  * the context's device and restores the calling thread's current device.  An
  * encoder/decoder handle is used by one thread at a time (like
  * &mut ReedSolomonEncoder).

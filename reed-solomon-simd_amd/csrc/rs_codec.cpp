@@ -188,7 +188,8 @@ struct rs_context {
     int device = 0;
     uint32_t *d_tw = nullptr;
     uint32_t *d_lut = nullptr;
-    uint16_t *d_lwfold = nullptr;
+    uint16_t *d_lwfold = nullptr;       // d_lwfold_base + 1 (segments 4-byte aligned)
+    uint16_t *d_lwfold_base = nullptr;
     uint16_t lw0 = 0;
     bool mono = true;             // RS_MI355X_NO_MONO=1 disables the column kernel
     bool split = true;            // RS_MI355X_NO_SPLIT=1 disables the split decode plan (A/B)
@@ -207,29 +208,64 @@ struct rs_context {
     std::mutex host_engine_mu;  // guards host_engine_buf (rs_engine_*_host staging)
     DevBuf host_engine_buf;
     std::mutex mu;  // guards ws_by_stream (device-resident API scratch), prof, recs
-    // at most RS_MAX_STREAM_WORKSPACES entries; the least recently used one is
-    // evicted (after a device synchronize: its stream may still use it, and the
-    // stream itself may already be destroyed) when a further stream arrives
+    // at most RS_MAX_STREAM_WORKSPACES entries.  When a further stream arrives,
+    // the least recently used entry's workspace is handed to it: first its
+    // `done` event (recorded on its stream at the end of each call that used it,
+    // ws_release) is waited for -- the event outlives a destroyed stream, and
+    // no other stream or context is stalled -- and its buffers are kept, so no
+    // hipFree (which synchronizes the device) runs on the call path
     struct WsEntry {
         std::unique_ptr<Workspace> w;
         uint64_t last_use = 0;
+        hipEvent_t done = nullptr;
+        bool done_valid = false;  // `done` was recorded after the entry's last call
     };
     std::unordered_map<hipStream_t, WsEntry> ws_by_stream;
     uint64_t ws_clock = 0;
     Workspace &ws(hipStream_t s) {  // caller holds mu, on the context's device
         auto it = ws_by_stream.find(s);
         if (it == ws_by_stream.end()) {
+            WsEntry e{std::unique_ptr<Workspace>(new Workspace), 0, nullptr, false};
             if (ws_by_stream.size() >= RS_MAX_STREAM_WORKSPACES) {
                 auto lru = ws_by_stream.begin();
                 for (auto j = ws_by_stream.begin(); j != ws_by_stream.end(); ++j)
                     if (j->second.last_use < lru->second.last_use) lru = j;
-                check(hipDeviceSynchronize());
+                if (lru->second.done_valid) check(hipEventSynchronize(lru->second.done));
+                else check(hipDeviceSynchronize());  // last used before the map filled up (see ws_release)
+                e.w = std::move(lru->second.w);
+                e.done = lru->second.done;
                 ws_by_stream.erase(lru);
             }
-            it = ws_by_stream.emplace(s, WsEntry{std::unique_ptr<Workspace>(new Workspace), 0}).first;
+            it = ws_by_stream.emplace(s, std::move(e)).first;
         }
         it->second.last_use = ++ws_clock;
         return *it->second.w;
+    }
+    // the call that used ws(s) has enqueued its work: mark the workspace busy
+    // until that completes (caller holds mu).  Only once the map is half full --
+    // an event record is one more packet on the caller's stream, and a caller
+    // with few streams never evicts
+    void ws_release(hipStream_t s) {
+        auto it = ws_by_stream.find(s);
+        if (it == ws_by_stream.end()) return;
+        WsEntry &e = it->second;
+        e.done_valid = false;
+        if (ws_by_stream.size() < RS_MAX_STREAM_WORKSPACES / 2) return;
+        if (!e.done && hipEventCreateWithFlags(&e.done, hipEventDisableTiming) != hipSuccess) {
+            e.done = nullptr;
+            return;
+        }
+        e.done_valid = hipEventRecord(e.done, s) == hipSuccess;
+    }
+    void ws_erase(hipStream_t s) {
+        auto it = ws_by_stream.find(s);
+        if (it == ws_by_stream.end()) return;
+        if (it->second.done) (void)hipEventDestroy(it->second.done);
+        ws_by_stream.erase(it);
+    }
+    ~rs_context() {
+        for (auto &kv : ws_by_stream)
+            if (kv.second.done) (void)hipEventDestroy(kv.second.done);
     }
     // kernel timing (rs_profile_enable)
     // host-memory pipeline (rs_encode_host / rs_decode_host), built on first use
@@ -265,6 +301,17 @@ struct rs_context {
 };
 
 namespace {
+// The workspace of one API call on stream s (caller holds ctx->mu); released
+// (rs_context::ws_release) once the call has enqueued its work.
+struct StreamWs {
+    rs_context *c;
+    hipStream_t s;
+    Workspace &w;
+    StreamWs(rs_context *c_, hipStream_t s_) : c(c_), s(s_), w(c_->ws(s_)) {}
+    ~StreamWs() { c->ws_release(s); }
+    StreamWs(const StreamWs &) = delete;
+    StreamWs &operator=(const StreamWs &) = delete;
+};
 // Kernel timing (rs_profile_enable): the context of the current API call.
 thread_local rs_context *t_prof_ctx = nullptr;
 struct ProfScope {
@@ -471,10 +518,15 @@ void launch_mono(int mode, uint32_t L, const rs::MonoArgs &M, hipStream_t s, uin
 // Single-level multi-chunk encodes: spread the chunks over the grid (grid.y)
 // when the packs alone give few workgroups (RS_MI355X_CHUNK_PARALLEL = 0 / 1
 // forces the serial / parallel form; tools/ab_chunks.sh measures the threshold).
+// The HighRate parallel form needs a work buffer of every chunk's IFFT rows
+// (`scratch` bytes, about the size of the input); past kChunkParallelMaxScratch
+// the serial form runs instead, which needs none (60000:100 x 32 KiB would
+// otherwise allocate ~1.9 GB per stream).
 constexpr uint32_t kChunkParallelMaxPacks = 4096;
-bool chunk_parallel(rs_context *ctx, const Geom &g) {
+constexpr uint64_t kChunkParallelMaxScratch = uint64_t(256) << 20;
+bool chunk_parallel(rs_context *ctx, const Geom &g, uint64_t scratch = 0) {
     if (ctx->chunk_par >= 0) return ctx->chunk_par != 0;
-    return g.packs <= kChunkParallelMaxPacks;
+    return g.packs <= kChunkParallelMaxPacks && scratch <= kChunkParallelMaxScratch;
 }
 
 // HighRate encode (rate_high.rs:44-87) from device rows to device rows:
@@ -510,7 +562,7 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
         launch_mono(rs::kMonoEncodeHigh, L, Mo, s, (N + M) * uint64_t(g.packs) * 8 * g.stripes);
         return;
     }
-    if (lv.m == 1 && (C == 1 || !chunk_parallel(ctx, g))) {
+    if (lv.m == 1 && (C == 1 || !chunk_parallel(ctx, g, uint64_t(C) * n * g.stride))) {
         A.src[0] = src;
         A.nsrc = 1;
         A.in_chunks = C;
@@ -940,15 +992,64 @@ const char *hip_msg(hipError_t e) { return hipGetErrorString(e); }
 // ===========================================================================
 // encoder / decoder objects
 
+// Host staging of the object API: pinned (the copies to and from the device
+// run asynchronously at the link's rate, with no bounce through a pageable
+// buffer), portable (any device's copies may use it: a work hand-off moves it
+// to a context on another GPU), grown monotonically, contents not kept.
+struct HostStage {
+    uint8_t *p = nullptr;
+    size_t cap = 0;
+    HostStage() = default;
+    HostStage(const HostStage &) = delete;
+    HostStage &operator=(const HostStage &) = delete;
+    uint8_t *get(size_t bytes) {
+        if (bytes > cap) {
+            if (p) check(hipHostFree(p));
+            p = nullptr;
+            cap = 0;
+            void *q = nullptr;
+            check(hipHostMalloc(&q, bytes ? bytes : 1, hipHostMallocPortable));
+            p = static_cast<uint8_t *>(q);
+            cap = bytes;
+        }
+        return p;
+    }
+    void swap(HostStage &o) {
+        std::swap(p, o.p);
+        std::swap(cap, o.cap);
+    }
+    ~HostStage() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+// The stream an encoder's / decoder's copies and kernels run on (created on
+// the object's device at its first encode / decode).
+struct ObjStream {
+    hipStream_t s = nullptr;
+    ObjStream() = default;
+    ObjStream(const ObjStream &) = delete;
+    ObjStream &operator=(const ObjStream &) = delete;
+    hipStream_t get() {  // on the object's device
+        if (!s) check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        return s;
+    }
+    void swap(ObjStream &o) { std::swap(s, o.s); }
+    ~ObjStream() {
+        if (s) (void)hipStreamDestroy(s);
+    }
+};
+
 struct rs_encoder {
     rs_context *ctx;
     rs_rate rate;
     bool high = true;
     uint64_t N = 0, M = 0, S = 0, row = 0, received = 0;
     bool has_result = false;
-    std::vector<uint8_t> h_orig, h_rec;  // padded rows / unpadded result
+    HostStage h_orig, h_rec;      // padded rows (64-byte blocks, shards.rs:38-59)
+    std::vector<uint8_t> h_tail;  // unpadded result when S % 64 != 0
     DevBuf d_orig, d_rec;
     Workspace ws;
+    ObjStream st;
 };
 
 struct rs_decoder {
@@ -959,45 +1060,53 @@ struct rs_decoder {
     uint64_t orig_received = 0, rec_received = 0;
     bool has_result = false, decoded = false;
     std::vector<uint8_t> orig_present, rec_present;
-    std::vector<uint8_t> h_orig, h_rec, h_out;
+    HostStage h_orig, h_rec, h_out;  // padded rows
+    std::vector<uint8_t> h_tail;     // unpadded restored rows when S % 64 != 0
     DevBuf d_orig, d_rec, d_out;
     Workspace ws;
+    ObjStream st;
 };
 
-// EncoderWork / DecoderWork (src/rate.rs:129-131, 206-208): an encoder's or
-// decoder's buffers, handed from one object to the next (any rate, any shape).
-// EncoderWork / DecoderWork: the buffers of an encoder / decoder handed from one
-// object to the next (rate.rs:129-139).  The device buffers (and the pinned
-// staging's event) belong to the device of the context that made them
-// (`device`): swap_host moves only the host buffers, for a context on another
-// device (device memory of GPU0 must not back GPU1's kernels).
+// EncoderWork / DecoderWork (src/rate.rs:129-139): the buffers of an encoder /
+// decoder handed from one object to the next (any rate, any shape).  The
+// device buffers, the stream (and the pinned staging's event) belong to the
+// device of the context that made them (`device`): swap_host moves only the
+// host buffers, for a context on another device (device memory of GPU0 must
+// not back GPU1's kernels).
 struct rs_encoder_work {
     int device = -1;
-    std::vector<uint8_t> h_orig, h_rec;
+    HostStage h_orig, h_rec;
+    std::vector<uint8_t> h_tail;
     DevBuf d_orig, d_rec;
     Workspace ws;
+    ObjStream st;
     void swap_host(rs_encoder &e) {
         h_orig.swap(e.h_orig);
         h_rec.swap(e.h_rec);
+        h_tail.swap(e.h_tail);
     }
     void swap(rs_encoder &e) {
         swap_host(e);
         d_orig.swap(e.d_orig);
         d_rec.swap(e.d_rec);
         ws.swap(e.ws);
+        st.swap(e.st);
     }
 };
 struct rs_decoder_work {
     int device = -1;
-    std::vector<uint8_t> orig_present, rec_present, h_orig, h_rec, h_out;
+    std::vector<uint8_t> orig_present, rec_present, h_tail;
+    HostStage h_orig, h_rec, h_out;
     DevBuf d_orig, d_rec, d_out;
     Workspace ws;
+    ObjStream st;
     void swap_host(rs_decoder &d) {
         orig_present.swap(d.orig_present);
         rec_present.swap(d.rec_present);
         h_orig.swap(d.h_orig);
         h_rec.swap(d.h_rec);
         h_out.swap(d.h_out);
+        h_tail.swap(d.h_tail);
     }
     void swap(rs_decoder &d) {
         swap_host(d);
@@ -1005,6 +1114,7 @@ struct rs_decoder_work {
         d_rec.swap(d.d_rec);
         d_out.swap(d.d_out);
         ws.swap(d.ws);
+        st.swap(d.st);
     }
 };
 
@@ -1052,8 +1162,11 @@ rs_status encoder_configure(rs_encoder *e, uint64_t N, uint64_t M, uint64_t S, r
     e->row = round_up(S, 64);
     e->received = 0;
     e->has_result = false;
-    e->h_orig.resize(N * e->row);
-    return set_err(err, RS_OK);
+    // pinned staging of the padded originals, written by add_original_shard
+    return guarded(err, [&]() -> rs_status {
+        e->h_orig.get(N * e->row);
+        return set_err(err, RS_OK);
+    });
 }
 
 rs_status decoder_configure(rs_decoder *d, uint64_t N, uint64_t M, uint64_t S, rs_error *err) {
@@ -1066,9 +1179,11 @@ rs_status decoder_configure(rs_decoder *d, uint64_t N, uint64_t M, uint64_t S, r
     d->has_result = d->decoded = false;
     d->orig_present.assign(N, 0);
     d->rec_present.assign(M, 0);
-    d->h_orig.resize(N * d->row);
-    d->h_rec.resize(M * d->row);
-    return set_err(err, RS_OK);
+    return guarded(err, [&]() -> rs_status {
+        d->h_orig.get(N * d->row);
+        d->h_rec.get(M * d->row);
+        return set_err(err, RS_OK);
+    });
 }
 
 void encoder_drop_result(rs_encoder *e) {
@@ -1103,7 +1218,11 @@ rs_status rs_context_create(int device, rs_context **out) {
         const rs::GfTables &T = rs::tables();
         check(hipMalloc(&ctx->d_tw, T.perm_by_skew.size() * 4));
         check(hipMalloc(&ctx->d_lut, T.perm_by_log.size() * 4));
-        check(hipMalloc(&ctx->d_lwfold, T.lw_fold.size() * 2));
+        // lw_fold's 2^u-entry segment starts at entry 2^u - 1 (gf_tables.hpp); one
+        // leading pad entry puts every segment of 2 or more entries on a 4-byte
+        // boundary (the column kernel reads a thread's pair as one dword)
+        check(hipMalloc(&ctx->d_lwfold_base, (T.lw_fold.size() + 1) * 2));
+        ctx->d_lwfold = ctx->d_lwfold_base + 1;
         check(hipMemcpy(ctx->d_tw, T.perm_by_skew.data(), T.perm_by_skew.size() * 4, hipMemcpyHostToDevice));
         check(hipMemcpy(ctx->d_lut, T.perm_by_log.data(), T.perm_by_log.size() * 4, hipMemcpyHostToDevice));
         check(hipMemcpy(ctx->d_lwfold, T.lw_fold.data(), T.lw_fold.size() * 2, hipMemcpyHostToDevice));
@@ -1122,7 +1241,8 @@ rs_status rs_context_create(int device, rs_context **out) {
         ctx->mono_all = ma && ma[0] == '1';
         if (const char *mp = getenv("RS_MI355X_MONO_MAX_PACKS")) ctx->mono_max_packs = uint32_t(strtoul(mp, nullptr, 10));
         if (const char *e2 = getenv("RS_MI355X_E2_MAX_PACKS")) ctx->e2_max_packs = uint32_t(strtoul(e2, nullptr, 10));
-        if (const char *cp = getenv("RS_MI355X_CHUNK_PARALLEL")) ctx->chunk_par = cp[0] == '1' ? 1 : 0;
+        if (const char *cp = getenv("RS_MI355X_CHUNK_PARALLEL"))  // "0" / "1"; anything else: automatic
+            ctx->chunk_par = cp[0] == '1' && !cp[1] ? 1 : cp[0] == '0' && !cp[1] ? 0 : -1;
         // column-kernel twiddle images of every transform size, built now: a lazy
         // build inside an asynchronous call would stall the device with a
         // synchronous upload the first time a size is seen
@@ -1146,7 +1266,7 @@ void rs_context_destroy(rs_context *ctx) {
     if (ctx->d_lut2) (void)hipFree(ctx->d_lut2);
     for (uint32_t *p : ctx->d_img2)
         if (p) (void)hipFree(p);
-    if (ctx->d_lwfold) (void)hipFree(ctx->d_lwfold);
+    if (ctx->d_lwfold_base) (void)hipFree(ctx->d_lwfold_base);
     for (uint32_t *p : ctx->d_img)
         if (p) (void)hipFree(p);
     delete ctx;
@@ -1199,10 +1319,11 @@ rs_status rs_encode_device_strided(rs_context *ctx, rs_rate rate, uint64_t N, ui
         ProfScope prof(ctx);
         const Geom g = device_geom(S, orig_stride, rec_stride, 0, {d_orig, d_rec});
         auto s = static_cast<hipStream_t>(stream);
+        StreamWs sw(ctx, s);
         if (high)
-            encode_high(ctx, ctx->ws(s), g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
+            encode_high(ctx, sw.w, g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
         else
-            encode_low(ctx, ctx->ws(s), g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
+            encode_low(ctx, sw.w, g, N, M, static_cast<const uint8_t *>(d_orig), static_cast<uint8_t *>(d_rec), s);
         return set_err(err, RS_OK);
     });
 }
@@ -1231,14 +1352,15 @@ rs_status rs_encode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint
         g.orig_bstride = orig_b;
         g.rec_bstride = rec_b;
         auto s = static_cast<hipStream_t>(stream);
+        StreamWs sw(ctx, s);
         for (uint64_t b0 = 0; b0 < stripes; b0 += kMaxBatchStripes) {  // grid.y limit
             g.stripes = uint32_t(std::min<uint64_t>(kMaxBatchStripes, stripes - b0));
             const uint8_t *o = static_cast<const uint8_t *>(d_orig) + b0 * orig_b;
             uint8_t *r = static_cast<uint8_t *>(d_rec) + b0 * rec_b;
             if (high)
-                encode_high(ctx, ctx->ws(s), g, N, M, o, r, s);
+                encode_high(ctx, sw.w, g, N, M, o, r, s);
             else
-                encode_low(ctx, ctx->ws(s), g, N, M, o, r, s);
+                encode_low(ctx, sw.w, g, N, M, o, r, s);
         }
         return set_err(err, RS_OK);
     });
@@ -1287,7 +1409,10 @@ void copy_rows(uint8_t *dst, const uint8_t *src, uint64_t pitch, uint64_t width,
         }
         uint64_t e = r + 1;
         while (e < rows && (!flag || (flag[e] != 0) == (want != 0))) ++e;
-        check(hipMemcpy2DAsync(dst + r * pitch, pitch, src + r * pitch, pitch, width, e - r, kind, s));
+        if (width == pitch)  // whole rows: one linear copy of the run
+            check(hipMemcpyAsync(dst + r * pitch, src + r * pitch, (e - r) * pitch, kind, s));
+        else
+            check(hipMemcpy2DAsync(dst + r * pitch, pitch, src + r * pitch, pitch, width, e - r, kind, s));
         r = e;
     }
 }
@@ -1406,7 +1531,8 @@ rs_status rs_decode_device_strided(rs_context *ctx, rs_rate rate, uint64_t N, ui
         DeviceGuard dg(ctx->device);
         ProfScope prof(ctx);
         const Geom g = device_geom(S, orig_stride, rec_stride, restored_stride, {d_orig, d_rec, d_restored});
-        decode_dev(ctx, ctx->ws(static_cast<hipStream_t>(stream)), high, g, N, M, static_cast<const uint8_t *>(d_orig), orig_present,
+        StreamWs sw(ctx, static_cast<hipStream_t>(stream));
+        decode_dev(ctx, sw.w, high, g, N, M, static_cast<const uint8_t *>(d_orig), orig_present,
                    static_cast<const uint8_t *>(d_rec), rec_present, static_cast<uint8_t *>(d_restored),
                    static_cast<hipStream_t>(stream));
         return set_err(err, RS_OK);
@@ -1451,9 +1577,10 @@ rs_status rs_decode_device_batch(rs_context *ctx, rs_rate rate, uint64_t N, uint
         g.out_bstride = restored_stripe_stride ? restored_stripe_stride : N * g.out();
         if ((g.orig_bstride | g.rec_bstride | g.out_bstride) % 4)
             g.fmt.io_bytes = 1, g.fmt.full_packs = uint32_t(S / 64 * 8), g.fmt.tail_h = uint32_t(S % 64 / 2);
+        StreamWs sw(ctx, static_cast<hipStream_t>(stream));
         for (uint64_t b0 = 0; b0 < stripes; b0 += kMaxBatchStripes) {  // grid.y limit
             g.stripes = uint32_t(std::min<uint64_t>(kMaxBatchStripes, stripes - b0));
-            decode_dev(ctx, ctx->ws(static_cast<hipStream_t>(stream)), high, g, N, M,
+            decode_dev(ctx, sw.w, high, g, N, M,
                        static_cast<const uint8_t *>(d_orig) + b0 * g.orig_bstride,
                        orig_present, static_cast<const uint8_t *>(d_rec) + b0 * g.rec_bstride, rec_present,
                        static_cast<uint8_t *>(d_restored) + b0 * g.out_bstride, static_cast<hipStream_t>(stream));
@@ -1509,7 +1636,7 @@ rs_status rs_encoder_add_original_shard(rs_encoder *e, const uint8_t *shard, uin
         if (err) err->shard_bytes = e->S, err->got = len;
         return RS_ERR_DIFFERENT_SHARD_SIZE;
     }
-    insert_row(&e->h_orig[e->received * e->row], shard, e->S);
+    insert_row(e->h_orig.p + e->received * e->row, shard, e->S);
     ++e->received;
     return set_err(err, RS_OK);
 }
@@ -1522,18 +1649,23 @@ rs_status rs_encoder_encode(rs_encoder *e, rs_error *err) {
         if (err) err->original_count = e->N, err->original_received_count = e->received;
         return RS_ERR_TOO_FEW_ORIGINAL_SHARDS;
     }
+    // one stream: pinned originals in, encode, pinned recovery rows out, one wait
     return guarded(err, [&]() -> rs_status {
         DeviceGuard dg(e->ctx->device);
+        const hipStream_t s = e->st.get();
         const Geom g{e->row, uint32_t(e->row / 8)};
         auto *d_orig = static_cast<uint8_t *>(e->d_orig.get(e->N * e->row));
         auto *d_rec = static_cast<uint8_t *>(e->d_rec.get(e->M * e->row));
-        check(hipMemcpy(d_orig, e->h_orig.data(), e->N * e->row, hipMemcpyHostToDevice));
-        if (e->high) encode_high(e->ctx, e->ws, g, e->N, e->M, d_orig, d_rec, nullptr);
-        else encode_low(e->ctx, e->ws, g, e->N, e->M, d_orig, d_rec, nullptr);
-        std::vector<uint8_t> padded(e->M * e->row);
-        check(hipMemcpy(padded.data(), d_rec, padded.size(), hipMemcpyDeviceToHost));
-        e->h_rec.resize(e->M * e->S);
-        for (uint64_t i = 0; i < e->M; ++i) extract_row(&e->h_rec[i * e->S], &padded[i * e->row], e->S);
+        uint8_t *h_rec = e->h_rec.get(e->M * e->row);
+        check(hipMemcpyAsync(d_orig, e->h_orig.p, e->N * e->row, hipMemcpyHostToDevice, s));
+        if (e->high) encode_high(e->ctx, e->ws, g, e->N, e->M, d_orig, d_rec, s);
+        else encode_low(e->ctx, e->ws, g, e->N, e->M, d_orig, d_rec, s);
+        check(hipMemcpyAsync(h_rec, d_rec, e->M * e->row, hipMemcpyDeviceToHost, s));
+        check(hipStreamSynchronize(s));
+        if (e->S != e->row) {  // tails: the reference's unpadded shards (shards.rs:62-74)
+            e->h_tail.resize(e->M * e->S);
+            for (uint64_t i = 0; i < e->M; ++i) extract_row(&e->h_tail[i * e->S], h_rec + i * e->row, e->S);
+        }
         e->has_result = true;
         return set_err(err, RS_OK);
     });
@@ -1541,7 +1673,7 @@ rs_status rs_encoder_encode(rs_encoder *e, rs_error *err) {
 
 const uint8_t *rs_encoder_recovery(rs_encoder *e, uint64_t index) {
     if (!e || !e->has_result || index >= e->M) return nullptr;
-    return &e->h_rec[index * e->S];
+    return e->S == e->row ? e->h_rec.p + index * e->row : &e->h_tail[index * e->S];
 }
 
 void rs_encoder_result_drop(rs_encoder *e) {
@@ -1621,7 +1753,7 @@ static rs_status dec_add(rs_decoder *d, bool orig, uint64_t index, const uint8_t
         if (err) err->shard_bytes = d->S, err->got = len;
         return RS_ERR_DIFFERENT_SHARD_SIZE;
     }
-    insert_row(&(orig ? d->h_orig : d->h_rec)[index * d->row], shard, d->S);
+    insert_row((orig ? d->h_orig : d->h_rec).p + index * d->row, shard, d->S);
     present[index] = 1;
     ++(orig ? d->orig_received : d->rec_received);
     return set_err(err, RS_OK);
@@ -1651,21 +1783,27 @@ rs_status rs_decoder_decode(rs_decoder *d, rs_error *err) {
         d->decoded = false;
         return set_err(err, RS_OK);
     }
+    // one stream: only received rows in, decode, only restored rows out, one wait
     return guarded(err, [&]() -> rs_status {
         DeviceGuard dg(d->ctx->device);
-        const Geom g{d->row, uint32_t(d->row / 8)};
-        auto *d_orig = static_cast<uint8_t *>(d->d_orig.get(d->N * d->row));
-        auto *d_rec = static_cast<uint8_t *>(d->d_rec.get(d->M * d->row));
-        auto *d_out = static_cast<uint8_t *>(d->d_out.get(d->N * d->row));
-        check(hipMemcpy(d_orig, d->h_orig.data(), d->N * d->row, hipMemcpyHostToDevice));
-        check(hipMemcpy(d_rec, d->h_rec.data(), d->M * d->row, hipMemcpyHostToDevice));
+        const hipStream_t s = d->st.get();
+        const uint64_t row = d->row;
+        const Geom g{row, uint32_t(row / 8)};
+        auto *d_orig = static_cast<uint8_t *>(d->d_orig.get(d->N * row));
+        auto *d_rec = static_cast<uint8_t *>(d->d_rec.get(d->M * row));
+        auto *d_out = static_cast<uint8_t *>(d->d_out.get(d->N * row));
+        uint8_t *h_out = d->h_out.get(d->N * row);
+        copy_rows(d_orig, d->h_orig.p, row, row, d->orig_present.data(), 1, d->N, hipMemcpyHostToDevice, s);
+        copy_rows(d_rec, d->h_rec.p, row, row, d->rec_present.data(), 1, d->M, hipMemcpyHostToDevice, s);
         decode_dev(d->ctx, d->ws, d->high, g, d->N, d->M, d_orig, d->orig_present.data(), d_rec,
-                   d->rec_present.data(), d_out, nullptr);
-        std::vector<uint8_t> padded(d->N * d->row);
-        check(hipMemcpy(padded.data(), d_out, padded.size(), hipMemcpyDeviceToHost));
-        d->h_out.assign(d->N * d->S, 0);
-        for (uint64_t i = 0; i < d->N; ++i)
-            if (!d->orig_present[i]) extract_row(&d->h_out[i * d->S], &padded[i * d->row], d->S);
+                   d->rec_present.data(), d_out, s);
+        copy_rows(h_out, d_out, row, row, d->orig_present.data(), 0, d->N, hipMemcpyDeviceToHost, s);
+        check(hipStreamSynchronize(s));
+        if (d->S != row) {  // tails: the reference's unpadded shards (shards.rs:62-74)
+            d->h_tail.resize(d->N * d->S);
+            for (uint64_t i = 0; i < d->N; ++i)
+                if (!d->orig_present[i]) extract_row(&d->h_tail[i * d->S], h_out + i * row, d->S);
+        }
         d->has_result = d->decoded = true;
         return set_err(err, RS_OK);
     });
@@ -1673,7 +1811,7 @@ rs_status rs_decoder_decode(rs_decoder *d, rs_error *err) {
 
 const uint8_t *rs_decoder_restored_original(rs_decoder *d, uint64_t index) {
     if (!d || !d->has_result || !d->decoded || index >= d->N || d->orig_present[index]) return nullptr;
-    return &d->h_out[index * d->S];
+    return d->S == d->row ? d->h_out.p + index * d->row : &d->h_tail[index * d->S];
 }
 
 uint64_t rs_decoder_restored_count(const rs_decoder *d) {
@@ -1722,7 +1860,8 @@ rs_status rs_encode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const u
     if (st != RS_OK) return st;
     for (uint64_t i = 0; i < given && st == RS_OK; ++i) st = rs_encoder_add_original_shard(e, original[i], S, err);
     if (st == RS_OK) st = rs_encoder_encode(e, err);
-    if (st == RS_OK && recovery_out) std::memcpy(recovery_out, e->h_rec.data(), M * S);
+    if (st == RS_OK && recovery_out)
+        for (uint64_t i = 0; i < M; ++i) std::memcpy(recovery_out + i * S, rs_encoder_recovery(e, i), S);
     rs_encoder_free(e);
     return st;
 }
@@ -1757,7 +1896,7 @@ rs_status rs_decode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const u
     if (st == RS_OK && d->decoded)
         for (uint64_t i = 0; i < N; ++i)
             if (!d->orig_present[i]) {
-                if (restored_out) std::memcpy(restored_out + i * S, &d->h_out[i * S], S);
+                if (restored_out) std::memcpy(restored_out + i * S, rs_decoder_restored_original(d, i), S);
                 if (restored_mask) restored_mask[i] = 1;
             }
     rs_decoder_free(d);
@@ -1832,7 +1971,8 @@ rs_status rs_engine_formal_derivative(rs_context *ctx, void *d_rows, uint64_t co
         DeviceGuard dg(ctx->device);
         const uint64_t bytes = count * len64 * 64;
         auto s = static_cast<hipStream_t>(stream);
-        auto *tmp = static_cast<uint8_t *>(ctx->ws(s).buf[0].get(bytes));
+        StreamWs sw(ctx, s);
+        auto *tmp = static_cast<uint8_t *>(sw.w.buf[0].get(bytes));
         check(hipMemcpyAsync(tmp, d_rows, bytes, hipMemcpyDeviceToDevice, s));
         check(rs::launch_formal_derivative(tmp, static_cast<uint8_t *>(d_rows), uint32_t(count), len64 * 64, s));
         return RS_OK;
@@ -1900,7 +2040,7 @@ rs_status rs_release_stream_scratch(rs_context *ctx, void *stream) {
         auto it = ctx->ws_by_stream.find(s);
         if (it == ctx->ws_by_stream.end()) return RS_OK;
         check(hipStreamSynchronize(s));
-        ctx->ws_by_stream.erase(it);
+        ctx->ws_erase(s);
         return RS_OK;
     });
 }

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 
 namespace rs {
@@ -80,6 +81,23 @@ __device__ __forceinline__ void st_word(uint8_t *p, uint32_t v, const PackIO &io
 #pragma unroll
     for (uint32_t e = 0; e < 4; ++e)
         if (e < io.cnt) p[e] = uint8_t(v >> (8 * e));
+}
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) of kernel `fn` on the
+// current device, once per device.  The attribute is per device, and one
+// process may drive several GPUs through several rs_contexts (each launcher
+// runs with its context's device current), so a process-wide flag would skip
+// every device after the first.  `done` is the kernel's own bit set of devices
+// (atomic: launchers run on many host threads).
+inline hipError_t lds_attr_once(std::atomic<uint64_t> &done, const void *fn, int bytes) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const uint64_t bit = dev >= 0 && dev < 64 ? uint64_t(1) << dev : 0;
+    if (bit && (done.load(std::memory_order_acquire) & bit)) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess && bit) done.fetch_or(bit, std::memory_order_acq_rel);
+    return e;
 }
 
 // One pass of the multi-pass transform (see DESIGN.md "Pass structure").

@@ -297,15 +297,13 @@ hipError_t launch_eval_poly(const EvalArgs &A, hipStream_t s) {
     if (A.u >= RS_EVAL_FAST_MIN_U && A.u <= 12) {
         static_assert((1u << 13) <= kEvalInlineRows, "k_eval_fast reads the inline bitmaps");
         const size_t lds = size_t(8) * n;  // two exchange buffers of 2^u words
-        static bool fast_attr = false;  // benign race: idempotent attribute calls
-        if (!fast_attr) {
-            for (const void *k : {reinterpret_cast<const void *>(&k_eval_fast<1>),
-                                  reinterpret_cast<const void *>(&k_eval_fast<2>),
-                                  reinterpret_cast<const void *>(&k_eval_fast<3>)}) {
-                hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
-                if (e != hipSuccess) return e;
-            }
-            fast_attr = true;
+        static std::atomic<uint64_t> fast_devs[3] = {{0}, {0}, {0}};  // per kernel: devices set
+        const void *kf[3] = {reinterpret_cast<const void *>(&k_eval_fast<1>),
+                             reinterpret_cast<const void *>(&k_eval_fast<2>),
+                             reinterpret_cast<const void *>(&k_eval_fast<3>)};
+        for (int k = 0; k < 3; ++k) {
+            hipError_t e = lds_attr_once(fast_devs[k], kf[k], 64 * 1024);
+            if (e != hipSuccess) return e;
         }
         if (A.u == 11) k_eval_fast<1><<<1, 1024, lds, s>>>(A);
         else if (A.u == 12) k_eval_fast<2><<<1, 1024, lds, s>>>(A);
@@ -327,12 +325,10 @@ hipError_t launch_eval_poly(const EvalArgs &A, hipStream_t s) {
         return hipGetLastError();
     }
     const size_t lds = size_t(2) * (n < 2 ? 2 : n) + size_t(8) * ((n + 31) / 32);
-    static bool attr_set = false;  // benign race: idempotent attribute call
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_eval_poly),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    static std::atomic<uint64_t> attr_devs{0};  // devices whose attribute is set
+    {
+        hipError_t e = lds_attr_once(attr_devs, reinterpret_cast<const void *>(&k_eval_poly), 160 * 1024);
         if (e != hipSuccess) return e;
-        attr_set = true;
     }
     const uint32_t threads = n / 2 >= 1024 ? 1024 : (n / 2 < 64 ? 64 : n / 2);
     k_eval_poly<<<1, threads, lds, s>>>(A);

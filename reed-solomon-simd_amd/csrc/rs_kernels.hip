@@ -741,12 +741,10 @@ template <int K, int LR, int SPL, int F>
 hipError_t launch_f(const PassArgs &A, hipStream_t s) {
     using P = Pass<K, LR, SPL>;
     const size_t lds = Lds<K, SPL, F>::bytes();
-    static bool attr_set = false;  // benign race: idempotent attribute call
-    if (!attr_set && lds > 65536) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pass<K, LR, SPL, F>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    static std::atomic<uint64_t> attr_devs{0};  // devices whose attribute is set
+    if (lds > 65536) {
+        hipError_t e = lds_attr_once(attr_devs, reinterpret_cast<const void *>(&k_pass<K, LR, SPL, F>), int(lds));
         if (e != hipSuccess) return e;
-        attr_set = true;
     }
     PassArgs B = A;
     B.slices = (A.packs + P::SP - 1) / P::SP;

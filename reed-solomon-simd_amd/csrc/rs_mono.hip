@@ -682,11 +682,15 @@ __device__ __forceinline__ uint32_t paired_row(uint32_t lane, uint32_t wave, int
 
 // Load transform rows `chunk * n + row` (placement: start of the IFFT) as
 // paired words; finish_col completes them.  Missing rows inside the caller's
-// matrices are read and discarded by the decode's scaling.
+// matrices are read and discarded by the decode's scaling.  okm bit j: word j
+// belongs to a row of the caller's matrices (others read a stand-in row and
+// are zeroed by finish_col, not here: a select on the loaded value would make
+// the compiler wait for the load right after issuing it)
 // (2-element packs: the paired words are the 16-bit low and high halves)
-template <int L, int LR, int SPLIT = 0, int E = 4>
+template <int L, int LR, int SPLIT = 0, int E = 4, int BYTES = -1>
 __device__ __forceinline__ void issue_col(const MonoCore &A, uint32_t chunk, const PackIO &io, const StripeBases &sb,
-                                          uint32_t (&w)[2 << LR], uint32_t lane, uint32_t wave, bool live = true) {
+                                          uint32_t (&w)[2 << LR], uint32_t &okm, uint32_t lane, uint32_t wave,
+                                          bool live = true) {
     using S = SeqOf<L, LR, false, SPLIT>;
     const uint32_t base = chunk * (1u << L);
     const uint32_t off = io.lo + ((lane & 1u) ? io.hi_delta : 0u);
@@ -696,13 +700,28 @@ __device__ __forceinline__ void issue_col(const MonoCore &A, uint32_t chunk, con
     // waits for OLDER loads (the decode's eval_poly inputs) count the loads in
     // it as absent and wait for these rows too
     const uint8_t *any_row = A.src[0].row_end > A.src[0].row_begin ? sb.src0 : sb.src1;
+    okm = 0;
+    // BYTES >= 0: the caller has branched on io.bytes (byte-wise packs: tails,
+    // unaligned matrices) around its whole prologue.  The decode must: a branch
+    // per row here joins a path whose bytes were combined as they landed, and
+    // at such joins the compiler copies the loaded words into shared registers
+    // -- reads that wait for every row load right after it is issued
+    const bool bytes = BYTES < 0 ? io.bytes : BYTES != 0;
+    PackIO q = io;
+    q.bytes = bytes;
     static_for<0, (2 << LR)>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         const uint32_t r = paired_row<S, 0, LR>(lane, wave, j) + base;
         const uint8_t *p = row_ptr(A, sb, r);
         const bool ok = p != nullptr && live;
-        uint32_t v = E == 4 ? ld_word((ok ? p : any_row) + off, io) : ld_half((ok ? p : any_row) + off, io);
-        v = ok ? v : 0u;
+        const uint8_t *a = (ok ? p : any_row) + off;
+        uint32_t v;
+        if constexpr (E == 4) v = ld_word(a, q);
+        else if (bytes) v = ld_half(a, q);
+        else  // the aligned dword holding the 16-bit half (finish_col picks it out: a
+              // zero-extending ushort load gets copied through an AND at the first join)
+            v = *reinterpret_cast<const uint32_t *>(a - (reinterpret_cast<uintptr_t>(a) & 3u));
+        okm |= uint32_t(ok) << j;
 #ifdef RS_MONO_SKIP_IO
         v = r * 0x9E3779B9u + off;
 #endif
@@ -801,14 +820,24 @@ __device__ __forceinline__ void scale_issue(const MonoCore &A, const uint32_t *r
 }
 
 template <int L, int LR, bool SCALE, int E>
-__device__ __forceinline__ void finish_col(uint32_t (&w)[2 << LR], const ScaleTabs<L, LR, E> *st, Col<L, LR, E> &c,
-                                           uint32_t lane) {
+__device__ __forceinline__ void finish_col(uint32_t (&w)[2 << LR], uint32_t okm, const ScaleTabs<L, LR, E> *st,
+                                           Col<L, LR, E> &c, uint32_t lane, const PackIO &io) {
+    // 2-element packs: a word holds its 16-bit half in bytes 0-1, or 2-3 when
+    // issue_col loaded the aligned dword around a half at offset 2 mod 4
+    const uint32_t sel = E == 2 && !io.bytes && (io.lo & 2u) ? 0x07060302u : 0x05040100u;
     constexpr int R = 1 << LR;
     static_for<0, R>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
+        // rows outside the caller's matrices are zero; a decode's are not
+        // received, so the scaling below zeroes them (the words of a lane pair
+        // hold one row: its garbage stays in that row)
+        if constexpr (!SCALE) {
+            w[2 * i] = (okm >> (2 * i)) & 1u ? w[2 * i] : 0u;
+            w[2 * i + 1] = (okm >> (2 * i + 1)) & 1u ? w[2 * i + 1] : 0u;
+        }
         xpose<0>(w[2 * i], w[2 * i + 1], lane);
         if constexpr (E == 2) {
-            c.lo[i] = w[2 * i] | (w[2 * i + 1] << 16);
+            c.lo[i] = __builtin_amdgcn_perm(w[2 * i + 1], w[2 * i], sel);
             if constexpr (SCALE) {
                 if constexpr (kQuadGather) c.lo[i] = quad_mul2(c.lo[i], st->t[i], lane);
                 else gf_mul2(c.lo[i], st->t[i]);
@@ -829,10 +858,11 @@ template <int L, int LR, bool SCALE>
 __device__ __forceinline__ void load_col(const MonoCore &A, uint32_t chunk, const PackIO &io, const StripeBases &sb,
                                          Col<L, LR> &c, uint32_t lane, uint32_t wave) {
     uint32_t w[2 << LR];
-    issue_col<L, LR>(A, chunk, io, sb, w, lane, wave);
+    uint32_t okm;
+    issue_col<L, LR>(A, chunk, io, sb, w, okm, lane, wave);
     ScaleTabs<L, LR> st;
     if constexpr (SCALE) scale_issue<L, LR>(A, A.rowinfo, st, lane, wave);
-    finish_col<L, LR, SCALE, 4>(w, &st, c, lane);
+    finish_col<L, LR, SCALE, 4>(w, okm, &st, c, lane, io);
 }
 
 // Reveal (decode, rate_high.rs:241-245): the multiply tables exp(65535 - log
@@ -1228,19 +1258,14 @@ __device__ __forceinline__ void col_walsh(uint32_t (&x)[2], uint32_t *buf) {
 
 // rinfo[r] = log factor | (received ? 0 : 0x10000) for the 2^L work rows.
 // ebits / rbits: this thread's erased / received bits (bits 0, 1 = rows 2t,
-// 2t+1); lw: lw_fold of those rows.  No barrier at the end (see the rinfo store).
-// s_waitcnt vmcnt(N) (a load the compiler does not track: see mono_body)
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-    static_assert(N >= 0 && N < 64, "vmcnt range");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// lwv: the thread's lw_fold pair (rows 2t, 2t + 1), loaded by inline asm with
-// NLIVE vector loads issued after it (NSKIP in a wave with `skip`).
-template <int L, int NLIVE, int NSKIP>
-__device__ __forceinline__ void col_eval_poly(const MonoCore &A, uint32_t ebits, uint32_t rbits, uint32_t lwv,
-                                              bool skip, uint32_t *buf, uint32_t *rinfo) {
+// 2t+1); lwv: lw_fold of those rows (two 16-bit values), an ordinary load the
+// compiler waits for at its first use below, after the first transform -- the
+// caller issues it first and calls this on straight-line code after its other
+// loads (mono_body), so that wait leaves them in flight.  No barrier at the end
+// (see the rinfo store).
+template <int L>
+__device__ __forceinline__ void col_eval_poly(const MonoCore &A, uint32_t ebits, uint32_t rbits, const uint32_t &lwv,
+                                              uint32_t *buf, uint32_t *rinfo) {
     const uint32_t i0 = 2 * threadIdx.x;
     uint32_t x[2];
     static_for<0, 2>([&](auto kc) {
@@ -1251,9 +1276,6 @@ __device__ __forceinline__ void col_eval_poly(const MonoCore &A, uint32_t ebits,
     });
     col_walsh<L, 0, 19>(x, buf);
     RS_MSTAMP(14);
-    if (skip) vm_wait<NSKIP>();
-    else vm_wait<NLIVE>();
-    RS_MSTAMP(15);
     const uint32_t lw[2] = {lwv & 0xFFFFu, lwv >> 16};
     static_for<0, 2>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
@@ -1452,307 +1474,327 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
     const uint32_t *img_d = A.img + uint64_t(ii ^ fi) * A.img_words;
     C c;
     if constexpr (STAGED) {
-        // one chunk in, one chunk out; every table read comes from LDS (layer
-        // 0 of phases 1 / 3 from the image when Stage::B0)
-        constexpr bool DEC = MODE == kMonoDecode;
-        uint32_t *shared = lds + G::plane_words;
-        // encodes fetch phase 3's tables from the FFT image (requested when phase 1
-        // ends); RS_MONO_ENC_DERIVE3: derive them in LDS from phase 1's (+ the D
-        // tables, Stage::kD) -- measured slower with the FLOW plan (profiles/r03j)
-        constexpr bool kDerive3 = !DEC && G::kDerive3;
-        constexpr uint32_t kSh = kDerive3 ? G::kShared + G::kD : G::kShared;  // shared tables (+ D)
-        uint32_t *priv = shared + kSh * G::SW + wave * G::kPriv * G::SW;
-        uint32_t *rinfo = lds + G::words;  // decode with fused eval_poly
-        constexpr uint32_t PC = G::PC;  // 16-byte pieces per table
-        constexpr int KP1 = (PC * G::kUp + 63) / 64;
-        constexpr int KP0 = G::B0 ? (PC * G::kL0 + 63) / 64 : 1;
-        constexpr int KP3 = G::kP3 ? (PC * G::kP3 + 63) / 64 : 1;  // (guarded by q < PC * kP3)
-        constexpr int KSH = kSh ? (PC * kSh + T - 1) / T : 1;  // (guarded by q < PC * kSh)
-        RS_MSTAMP(0);
-        // decode: does this wave's phase-1 row block (2^IW consecutive rows) hold a
-        // received row?  If not its rows are zero through phase 1: it loads no
-        // rows and no phase-1 tables, and skips the phase-1 layers
-        bool live = true;
-        if constexpr (DEC) {
-            static_assert(!STAGED || (1u << G::IW) / 32 == 4, "a wave's phase-1 rows: its 4 bitmap words");
-            live = (rw[0] | rw[1] | rw[2] | rw[3]) != 0;
-        }
-        // split decode: does this wave's half go on with the FFT (restored rows)?
-        const bool out_wave = !SPLIT || (wave >> (L - 1 - G::IW)) == A.out_half;
-        // Phase 3's tables cover the same wave rows, layers and slots as phase
-        // 1's, still in the region when phase 1 ran on real tables (live): the
-        // same tables when IFFT and FFT share the skew offset (decodes,
-        // rate_high.rs:213-245), else phase 1's XOR D_b (encodes, Stage::kD)
-#ifndef RS_MONO_NO_REUSE
-        const bool same3 = A.ifft_img == A.fft_img;
-        const bool reuse3 = live && (same3 || kDerive3);
-#else
-        const bool same3 = A.ifft_img == A.fft_img;
-        const bool reuse3 = false;
-#endif
-
-        // every global read is requested before any of them is waited for.
-        // Decodes: eval_poly's inputs first.  Thread t's erased / received bits
-        // (rows 2t, 2t + 1) are in word t / 16 of the bitmaps: the wave's 4 words
-        // are uniform, i.e. scalar loads of the kernel arguments.  Its lw_fold
-        // pair is the first vector load, issued by inline asm, so the compiler's
-        // vmcnt waits do not know it: col_eval_poly waits for it by an explicit
-        // count of the vector loads issued after it (rows and table pieces, all
-        // unconditional), leaving those in flight while eval_poly runs
-        uint32_t ebits = 0, rbits = 0, lwv = 0;
-        if constexpr (DEC) {  // the staged decode always evaluates eval_poly itself
-            const uint32_t g = lane >> 4, sh = (2u * lane) & 31u;
-            const uint32_t e0 = ew[0], e1 = ew[1], e2 = ew[2], e3 = ew[3], r0 = rw[0], r1 = rw[1], r2 = rw[2], r3 = rw[3];
-            ebits = (g == 0 ? e0 : g == 1 ? e1 : g == 2 ? e2 : e3) >> sh;
-            rbits = (g == 0 ? r0 : g == 1 ? r1 : g == 2 ? r2 : r3) >> sh;
-            // (lw_fold + 2t: 2-byte aligned; the compiler's own merged loads of it
-            // are the same unaligned dword access)
-            asm volatile("global_load_dword %0, %1, off" : "=v"(lwv) : "v"(A.lw_fold + 2u * threadIdx.x) : "memory");
-        }
-        // Decodes: a wave whose phase-1 rows hold no received row (!live) loads
-        // no rows, no phase-1 tables and no scale tables (uniform branches: the
-        // vector-memory issue rate of the ~330 load instructions of a 2^11-row
-        // workgroup bounds the prologue, and 7 of 16 waves are not live at 1 %)
-#ifndef RS_MONO_DEC_LOAD_ALL
-        const bool skip = DEC && !live;
-#else
-        const bool skip = false;
-#endif
-        uint32_t w[2 << LR] = {};
-        auto issue_rows = [&]() { issue_col<L, LR, PK, E>(A, 0, io, sb, w, lane, wave, live); };
-        // phase-1 tables (a live wave loads all of its region's pieces; lanes past
-        // the region's end re-read its last piece and do not write it, so the
-        // loads are unconditional); B0: layer 0's go into the region first, the
-        // layers above when layer 0 has read them (run_seq's hook)
-        uint4 v0[KP0], v1[KP1], vs[KSH];
-        auto issue_priv = [&]() {
-#ifndef RS_MONO_SKIP_STAGE  // tools/mono_probe.hip ablation
-            if constexpr (G::B0)
-                static_for<0, KP0>([&](auto kc) {
-                    const uint32_t q = clamp_piece(lane + 64u * decltype(kc)::value, PC * G::kL0);
-                    v0[kc] = l0_piece<L, LR, PK, E>(img_i, wave, live ? q : q % PC);
-                });
-            static_for<0, KP1>([&](auto kc) {
-                const uint32_t q = clamp_piece(lane + 64u * decltype(kc)::value, PC * G::kUp);
-                v1[kc] = priv_piece<L, LR, PK, E>(img_i, wave, live ? q : q % PC);
-            });
-#endif
-        };
-        // the shared region: every thread of the workgroup loads and writes pieces
-        auto issue_shared = [&]() {
-#ifndef RS_MONO_SKIP_STAGE
-            if constexpr (kSh > 0)
-                static_for<0, KSH>([&](auto kc) {
-                    const uint32_t q = clamp_piece(threadIdx.x + T * decltype(kc)::value, PC * kSh);
-                    if constexpr (kSh == G::kShared) {
-                        vs[kc] = ld_piece(shared_piece_ptr<L, LR, PK, E>(img_i, img_f, q));
-                    } else {
-                        const uint4 *src = q < PC * G::kShared ? shared_piece_ptr<L, LR, PK, E>(img_i, img_f, q)
-                                                               : d_piece_ptr<L, LR, PK, E>(img_d, q - PC * G::kShared);
-                        vs[kc] = ld_piece(src);
-                    }
-                });
-#endif
-        };
-#ifndef RS_MONO_SKIP_STAGE
-        constexpr int kPrivLoads = (G::B0 ? KP0 : 0) + KP1, kShLoads = kSh > 0 ? KSH : 0;
-#else
-        constexpr int kPrivLoads = 0, kShLoads = 0;
-#endif
-        constexpr int kRowLoads = 2 << LR;
-        // Decodes, order of the loads around eval_poly (inputs first, see above).
-        // RS_MONO_DEC_ORDER 1: the shared tables, the live waves' rows and phase-1
-        // tables, all in flight while eval_poly runs, then the scale gathers;
-        // 2: rows, eval_poly, gathers, then the tables; 3: shared tables and rows,
-        // eval_poly, gathers, phase-1 tables
-#ifndef RS_MONO_DEC_ORDER
-#define RS_MONO_DEC_ORDER 1
-#endif
-        constexpr int kOrder = RS_MONO_DEC_ORDER;
-        // 4: the shared tables only, eval_poly, then rows, gathers, phase-1 tables
-        constexpr bool kShFirst = kOrder != 2, kPrivFirst = kOrder == 1, kRowsFirst = kOrder != 4;
-        if constexpr (!DEC) {
-            issue_rows();
-            issue_priv();
-            issue_shared();
-        } else {
-            if constexpr (kShFirst) issue_shared();
-            RS_MSTAMP(16);
-            if (!skip) {
-                if constexpr (kRowsFirst) issue_rows();
-                RS_MSTAMP(17);
-                if constexpr (kPrivFirst) issue_priv();
+      // kBytesIO (staged decodes): the pack's row access form, byte-wise (1: tails,
+      // unaligned matrices) or not (0), as a compile-time branch around the whole
+      // body -- a join of the two forms' row loads makes the compiler copy the loaded
+      // words, and those copies wait for the loads (issue_col); -1: decided per load
+      auto staged = [&](auto bytes_c) {
+        constexpr int kBytesIO = decltype(bytes_c)::value;
+            // one chunk in, one chunk out; every table read comes from LDS (layer
+            // 0 of phases 1 / 3 from the image when Stage::B0)
+            constexpr bool DEC = MODE == kMonoDecode;
+            uint32_t *shared = lds + G::plane_words;
+            // encodes fetch phase 3's tables from the FFT image (requested when phase 1
+            // ends); RS_MONO_ENC_DERIVE3: derive them in LDS from phase 1's (+ the D
+            // tables, Stage::kD) -- measured slower with the FLOW plan (commit 7f40027: probe 8.27 -> 7.90 us
+            // per headline launch with fetched tables)
+            constexpr bool kDerive3 = !DEC && G::kDerive3;
+            constexpr uint32_t kSh = kDerive3 ? G::kShared + G::kD : G::kShared;  // shared tables (+ D)
+            uint32_t *priv = shared + kSh * G::SW + wave * G::kPriv * G::SW;
+            uint32_t *rinfo = lds + G::words;  // decode with fused eval_poly
+            constexpr uint32_t PC = G::PC;  // 16-byte pieces per table
+            constexpr int KP1 = (PC * G::kUp + 63) / 64;
+            constexpr int KP0 = G::B0 ? (PC * G::kL0 + 63) / 64 : 1;
+            constexpr int KP3 = G::kP3 ? (PC * G::kP3 + 63) / 64 : 1;  // (guarded by q < PC * kP3)
+            constexpr int KSH = kSh ? (PC * kSh + T - 1) / T : 1;  // (guarded by q < PC * kSh)
+            RS_MSTAMP(0);
+            // decode: does this wave's phase-1 row block (2^IW consecutive rows) hold a
+            // received row?  If not its rows are zero through phase 1: it loads no
+            // rows and no phase-1 tables, and skips the phase-1 layers
+            bool live = true;
+            if constexpr (DEC) {
+                static_assert(!STAGED || (1u << G::IW) / 32 == 4, "a wave's phase-1 rows: its 4 bitmap words");
+                live = (rw[0] | rw[1] | rw[2] | rw[3]) != 0;
             }
-            RS_MSTAMP(18);
-        }
-        const uint32_t *ri = A.rowinfo;
-        if constexpr (DEC) {
-            // vector loads issued after lw_fold's (see above), per branch
-            constexpr int kAfterSkip = kShFirst ? kShLoads : 0;
-            constexpr int kAfterLive = kAfterSkip + (kRowsFirst ? kRowLoads : 0) + (kPrivFirst ? kPrivLoads : 0);
-#ifndef RS_MONO_SKIP_EVAL  // tools/mono_probe.hip ablation
-            col_eval_poly<L, kAfterLive, kAfterSkip>(A, ebits, rbits, lwv, skip, plane, rinfo);
-#else
-            if (skip) vm_wait<kAfterSkip>();
-            else vm_wait<kAfterLive>();
-            rinfo[2 * threadIdx.x] = ebits & 1u ? 0x10000u : lwv & 0xFFFFu;
-            rinfo[2 * threadIdx.x + 1] = ebits & 2u ? 0x10000u : lwv >> 16;
-            __syncthreads();
-#endif
-            ri = rinfo;
-            RS_MSTAMP(2);
-        }
-        ScaleTabs<L, LR, E> st;
-        // (decodes) the scale gathers go out as soon as eval_poly is done
-        if constexpr (DEC) {
-            if constexpr (!kRowsFirst)
-                if (!skip) issue_rows();
-            scale_issue<L, LR, PK, E>(A, ri, st, lane, wave, !skip);
-            if constexpr (!kShFirst) issue_shared();
-            if constexpr (!kPrivFirst)
-                if (!skip) issue_priv();
-        }
-        RS_MSTAMP(13);
-        auto write1 = [&]() {
-#ifndef RS_MONO_SKIP_STAGE
-            static_for<0, KP1>([&](auto kc) {
-                const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < PC * G::kUp) reinterpret_cast<uint4 *>(priv)[G::at1(q)] = v1[kc];
-            });
-#endif
-        };
-#ifndef RS_MONO_SKIP_STAGE
-        if (!skip) {  // (a skipping wave's region is written by phase 3's tables before use)
-            if constexpr (G::B0)
-                static_for<0, KP0>([&](auto kc) {
-                    const uint32_t q = lane + 64u * decltype(kc)::value;
-                    if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at0(q)] = v0[kc];
+            // split decode: does this wave's half go on with the FFT (restored rows)?
+            bool out_wave = true;
+            if constexpr (SPLIT) out_wave = (wave >> (L - 1 - G::IW)) == A.out_half;
+            // Phase 3's tables cover the same wave rows, layers and slots as phase
+            // 1's, still in the region when phase 1 ran on real tables (live): the
+            // same tables when IFFT and FFT share the skew offset (decodes,
+            // rate_high.rs:213-245), else phase 1's XOR D_b (encodes, Stage::kD)
+    #ifndef RS_MONO_NO_REUSE
+            const bool same3 = A.ifft_img == A.fft_img;
+            const bool reuse3 = live && (same3 || kDerive3);
+    #else
+            const bool same3 = A.ifft_img == A.fft_img;
+            const bool reuse3 = false;
+    #endif
+
+            // every global read is requested before any of them is waited for.
+            // Decodes: eval_poly's inputs first.  Thread t's erased / received bits
+            // (rows 2t, 2t + 1) are in word t / 16 of the bitmaps: the wave's 4 words
+            // are uniform, i.e. scalar loads of the kernel arguments.  Its lw_fold
+            // pair is the first vector load, issued by inline asm, so the compiler's
+            // vmcnt waits do not know it: col_eval_poly waits for it by an explicit
+            // count of the vector loads issued after it (rows and table pieces, all
+            // unconditional), leaving those in flight while eval_poly runs
+            uint32_t ebits = 0, rbits = 0, lwv = 0;
+            if constexpr (DEC) {  // the staged decode always evaluates eval_poly itself
+                const uint32_t g = lane >> 4, sh = (2u * lane) & 31u;
+                const uint32_t e0 = ew[0], e1 = ew[1], e2 = ew[2], e3 = ew[3], r0 = rw[0], r1 = rw[1], r2 = rw[2], r3 = rw[3];
+                ebits = (g == 0 ? e0 : g == 1 ? e1 : g == 2 ? e2 : e3) >> sh;
+                rbits = (g == 0 ? r0 : g == 1 ? r1 : g == 2 ? r2 : r3) >> sh;
+                // lw_fold of rows 2t, 2t + 1 as one dword (the context keeps every
+                // 2^u-entry segment 4-byte aligned, rs_codec.cpp rs_context_create)
+                lwv = reinterpret_cast<const uint32_t *>(A.lw_fold)[threadIdx.x];
+                asm volatile("" ::: "memory");  // issued first, ahead of every other load
+            }
+            // Decodes: a wave whose phase-1 rows hold no received row (!live) loads
+            // no rows, no phase-1 tables and no scale tables (uniform branches: the
+            // vector-memory issue rate of the ~330 load instructions of a 2^11-row
+            // workgroup bounds the prologue, and 7 of 16 waves are not live at 1 %)
+    #ifndef RS_MONO_DEC_LOAD_ALL
+            const bool skip = DEC && !live;
+    #else
+            const bool skip = false;
+    #endif
+            uint32_t w[2 << LR] = {};
+            uint32_t okm = 0;
+            auto issue_rows = [&](auto bytes) {
+                issue_col<L, LR, PK, E, decltype(bytes)::value>(A, 0, io, sb, w, okm, lane, wave, live);
+            };
+            // phase-1 tables (a live wave loads all of its region's pieces; lanes past
+            // the region's end re-read its last piece and do not write it, so the
+            // loads are unconditional); B0: layer 0's go into the region first, the
+            // layers above when layer 0 has read them (run_seq's hook)
+            uint4 v0[KP0], v1[KP1], vs[KSH];
+            auto issue_priv = [&]() {
+    #ifndef RS_MONO_SKIP_STAGE  // tools/mono_probe.hip ablation
+                if constexpr (G::B0)
+                    static_for<0, KP0>([&](auto kc) {
+                        const uint32_t q = clamp_piece(lane + 64u * decltype(kc)::value, PC * G::kL0);
+                        v0[kc] = l0_piece<L, LR, PK, E>(img_i, wave, live ? q : q % PC);
+                    });
+                static_for<0, KP1>([&](auto kc) {
+                    const uint32_t q = clamp_piece(lane + 64u * decltype(kc)::value, PC * G::kUp);
+                    v1[kc] = priv_piece<L, LR, PK, E>(img_i, wave, live ? q : q % PC);
                 });
-            else
-                write1();
-        }
-        static_for<0, KSH>([&](auto kc) {
-            const uint32_t q = threadIdx.x + T * decltype(kc)::value;
-            if (q < PC * kSh) reinterpret_cast<uint4 *>(shared)[G::atS(q)] = vs[kc];
-        });
-#endif
-        finish_col<L, LR, DEC>(w, &st, c, lane);
-        RS_MSTAMP(1);
-        const LdsTabs<L, LR, PK, E> ts{priv, shared, img_i, img_f};
-        // phase-3 tables: requested when phase 1 ends, written over this wave's
-        // phase-1 tables when phase 2 ends
-        uint4 v3[KP3];
-        auto issue3 = [&]() {
-            if (reuse3) return;
-            if constexpr (G::kP3 > 0)
-            static_for<0, KP3>([&](auto kc) {
-                const uint32_t q = lane + 64u * decltype(kc)::value;
-                const uint32_t qc = clamp_piece(q, PC * G::kP3);
-                v3[kc] = priv_piece<L, LR, PK, E>(img_f, wave, out_wave ? qc : qc % PC);
-            });
-        };
-        auto write3 = [&]() {
-            if (reuse3) {
-                if constexpr (kDerive3) {
-                    if (same3) return;
-                    uint4 x[KP3];
-                    static_for<0, KP3>([&](auto kc) {
-                        const uint32_t q = lane + 64u * decltype(kc)::value;
-                        if (q < PC * G::kP3) {
-                            const uint32_t t = q / PC, piece = q - t * PC;
-                            const uint4 v = reinterpret_cast<const uint4 *>(priv)[G::at1(q)];
-                            const uint4 d = reinterpret_cast<const uint4 *>(shared)[(G::kShared + priv_layer<L, LR, PK, E>(t)) * G::SPC + piece];
-                            x[kc] = uint4{v.x ^ d.x, v.y ^ d.y, v.z ^ d.z, v.w ^ d.w};
+    #endif
+            };
+            // the shared region: every thread of the workgroup loads and writes pieces
+            auto issue_shared = [&]() {
+    #ifndef RS_MONO_SKIP_STAGE
+                if constexpr (kSh > 0)
+                    static_for<0, KSH>([&](auto kc) {
+                        const uint32_t q = clamp_piece(threadIdx.x + T * decltype(kc)::value, PC * kSh);
+                        if constexpr (kSh == G::kShared) {
+                            vs[kc] = ld_piece(shared_piece_ptr<L, LR, PK, E>(img_i, img_f, q));
+                        } else {
+                            const uint4 *src = q < PC * G::kShared ? shared_piece_ptr<L, LR, PK, E>(img_i, img_f, q)
+                                                                   : d_piece_ptr<L, LR, PK, E>(img_d, q - PC * G::kShared);
+                            vs[kc] = ld_piece(src);
                         }
                     });
-                    static_for<0, KP3>([&](auto kc) {
-                        const uint32_t q = lane + 64u * decltype(kc)::value;
-                        if (q < PC * G::kP3) reinterpret_cast<uint4 *>(priv)[G::at1(q)] = x[kc];
-                    });
-                }
-                return;
-            }
-            static_for<0, KP3>([&](auto kc) {
-                const uint32_t q = lane + 64u * decltype(kc)::value;
-                if (q < PC * G::kP3) reinterpret_cast<uint4 *>(priv)[G::at1(q)] = v3[kc];
-            });
-        };
-        // B0: the FFT's layer-0 tables (phase 3's last layer), requested while the
-        // FFT's phase 2 runs, take their turn in the region before that layer
-        uint4 v4[KP0];
-        auto issue4 = [&](bool need) {
-            if constexpr (G::B0)
-                static_for<0, KP0>([&](auto kc) {
-                    const uint32_t q = lane + 64u * decltype(kc)::value;
-                    const uint32_t qc = clamp_piece(q, PC * G::kL0);
-                    v4[kc] = l0_piece<L, LR, PK, E>(img_f, wave, need ? qc : qc % PC);
-                });
-        };
-        auto write4 = [&]() {
-            if constexpr (G::B0)
-                static_for<0, KP0>([&](auto kc) {
-                    const uint32_t q = lane + 64u * decltype(kc)::value;
-                    if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at0(q)] = v4[kc];
-                });
-        };
-        // 2-element decodes: the reveal tables are requested just before the FFT's
-        // last remap (with phase 3's table writes), so they land while phase 3 runs
-        constexpr bool kPreReveal = DEC && E == 2 && kQuadGather;
-        RevealTabs<LR> rt;
-        auto pre3 = [&](bool alive) {
-            return [&, alive]() {
-                write3();
-                if constexpr (kPreReveal)
-                    if (alive) reveal_issue<L, LR, PK>(A, ri, rt, lane, wave);
+    #endif
             };
-        };
-        if constexpr (SPLIT) {
-            // the wave's half: the highest wave bit in both placements
-            constexpr uint32_t kHalfWords = (G::n / 2) / 32;
-            uint32_t half_any = 0;
-            const uint32_t h = wave >> (L - 1 - G::IW);
-            for (uint32_t k = 0; k < kHalfWords; ++k) half_any |= K.received[h * kHalfWords + k];
-            // IFFT: a wave whose rows hold no received row skips phase 1 (its rows
-            // stay zero), a half without received rows skips phase 2
-            run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 1 : -1, PK>(ts, c, plane, lane, wave, issue3,
-                                                                         half_any != 0, live, write1);
-            RS_MSTAMP(5);
-            using SF = SeqOf<L, LR, true, PK>;
-            constexpr int NLF = num_layers(SF::v);
-            const bool out = out_wave;
-            const bool alive = out && wave_stores<L, LR, PK>(A, wave);
-            constexpr uint32_t kTopI = (G::n >> G::IW) - 2, kTopF = G::kShI + (G::n >> G::FLO) - 2;
-            split_top<L, LR>(c, plane, lds + G::words_dec, shared + kTopI * G::SW, shared + kTopF * G::SW, lane, wave,
-                             A.out_half);
-            RS_MSTAMP(6);
-            issue4(alive);
-            // FFT below the top layer: only the half that holds restored rows
-            run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, PK>(ts, c, plane, lane, wave, pre3(alive),
-                                                                              alive, out, write4);
-            if (!alive) return;
-        } else if constexpr (G::WB > 0) {
-            run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 1 : -1, PK>(ts, c, plane, lane, wave, issue3, true, live,
-                                                                   write1);
-            RS_MSTAMP(5);
-            using SF = SeqOf<L, LR, true, PK>;
-            constexpr int NLF = num_layers(SF::v);
-            const bool alive = !DEC || wave_stores<L, LR, PK>(A, wave);
-            issue4(alive);  // (waves that stop early all read one table: no branch around the loads)
-            if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
-            run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, PK>(ts, c, plane, lane, wave, pre3(alive), alive,
-                                                                        true, write4);
-            if (!alive) return;
-        } else {
-            static_assert(!G::B0, "one-segment plans keep every table in the region");
-            run_seq<L, LR, false, RS_MONO_LDS_PF, -1, PK>(ts, c, plane, lane, wave, NoHook{});
-            issue3();
-            if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
-            write3();
-            run_seq<L, LR, true, RS_MONO_LDS_PF, -1, PK>(ts, c, plane, lane, wave, NoHook{});
-        }
-        RS_MSTAMP(10);
-        store_col<L, LR, DEC, PK>(A, ri, 0, io, sb, c, lane, wave, kPreReveal && G::WB > 0 ? &rt : nullptr);
-        RS_MSTAMP(11);
+            // Decodes, order of the loads around eval_poly (inputs first, see above).
+            // RS_MONO_DEC_ORDER 1: the shared tables, the live waves' rows and phase-1
+            // tables, all in flight while eval_poly runs, then the scale gathers;
+            // 2: rows, eval_poly, gathers, then the tables; 3: shared tables and rows,
+            // eval_poly, gathers, phase-1 tables
+    #ifndef RS_MONO_DEC_ORDER
+    #define RS_MONO_DEC_ORDER 1
+    #endif
+            constexpr int kOrder = RS_MONO_DEC_ORDER;
+            // 4: the shared tables only, eval_poly, then rows, gathers, phase-1 tables
+            constexpr bool kShFirst = kOrder != 2, kPrivFirst = kOrder == 1, kRowsFirst = kOrder != 4;
+            const uint32_t *ri = A.rowinfo;
+            // eval_poly (decodes): the compiler places the wait for lwv at its first
+            // use, counting the loads issued since on the path that reaches it; with
+            // the row and table loads behind a branch (skipping waves issue none) a
+            // wait after the join would have to assume the fewer loads of the skip
+            // path and hold live waves until their rows land -- so each path gets its
+            // own copy of eval_poly, on straight-line code after its loads
+            auto eval = [&]() {
+    #ifndef RS_MONO_SKIP_EVAL  // tools/mono_probe.hip ablation
+                col_eval_poly<L>(A, ebits, rbits, lwv, plane, rinfo);
+    #else
+                rinfo[2 * threadIdx.x] = ebits & 1u ? 0x10000u : lwv & 0xFFFFu;
+                rinfo[2 * threadIdx.x + 1] = ebits & 2u ? 0x10000u : lwv >> 16;
+                __syncthreads();
+    #endif
+            };
+            using kIO = std::integral_constant<int, kBytesIO>;
+            if constexpr (!DEC) {
+                issue_rows(kIO{});
+                issue_priv();
+                issue_shared();
+            } else {
+                if constexpr (kShFirst) issue_shared();
+                RS_MSTAMP(16);
+                if (skip) {
+                    RS_MSTAMP(18);
+                    eval();
+                } else {
+                    if constexpr (kRowsFirst) issue_rows(kIO{});
+                    RS_MSTAMP(17);
+                    if constexpr (kPrivFirst) issue_priv();
+                    RS_MSTAMP(18);
+                    eval();
+                }
+                ri = rinfo;
+                RS_MSTAMP(2);
+            }
+            ScaleTabs<L, LR, E> st;
+            // (decodes) the scale gathers go out as soon as eval_poly is done
+            if constexpr (DEC) {
+                if constexpr (!kRowsFirst)
+                    if (!skip) issue_rows(kIO{});
+                scale_issue<L, LR, PK, E>(A, ri, st, lane, wave, !skip);
+                if constexpr (!kShFirst) issue_shared();
+                if constexpr (!kPrivFirst)
+                    if (!skip) issue_priv();
+            }
+            RS_MSTAMP(13);
+            auto write1 = [&]() {
+    #ifndef RS_MONO_SKIP_STAGE
+                static_for<0, KP1>([&](auto kc) {
+                    const uint32_t q = lane + 64u * decltype(kc)::value;
+                    if (q < PC * G::kUp) reinterpret_cast<uint4 *>(priv)[G::at1(q)] = v1[kc];
+                });
+    #endif
+            };
+    #ifndef RS_MONO_SKIP_STAGE
+            if (!skip) {  // (a skipping wave's region is written by phase 3's tables before use)
+                if constexpr (G::B0)
+                    static_for<0, KP0>([&](auto kc) {
+                        const uint32_t q = lane + 64u * decltype(kc)::value;
+                        if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at0(q)] = v0[kc];
+                    });
+                else
+                    write1();
+            }
+            static_for<0, KSH>([&](auto kc) {
+                const uint32_t q = threadIdx.x + T * decltype(kc)::value;
+                if (q < PC * kSh) reinterpret_cast<uint4 *>(shared)[G::atS(q)] = vs[kc];
+            });
+    #endif
+            finish_col<L, LR, DEC>(w, okm, &st, c, lane, io);
+            RS_MSTAMP(1);
+            const LdsTabs<L, LR, PK, E> ts{priv, shared, img_i, img_f};
+            // phase-3 tables: requested when phase 1 ends, written over this wave's
+            // phase-1 tables when phase 2 ends
+            uint4 v3[KP3];
+            auto issue3 = [&]() {
+                if (reuse3) return;
+                if constexpr (G::kP3 > 0)
+                static_for<0, KP3>([&](auto kc) {
+                    const uint32_t q = lane + 64u * decltype(kc)::value;
+                    const uint32_t qc = clamp_piece(q, PC * G::kP3);
+                    v3[kc] = priv_piece<L, LR, PK, E>(img_f, wave, out_wave ? qc : qc % PC);
+                });
+            };
+            auto write3 = [&]() {
+                if (reuse3) {
+                    if constexpr (kDerive3) {
+                        if (same3) return;
+                        uint4 x[KP3];
+                        static_for<0, KP3>([&](auto kc) {
+                            const uint32_t q = lane + 64u * decltype(kc)::value;
+                            if (q < PC * G::kP3) {
+                                const uint32_t t = q / PC, piece = q - t * PC;
+                                const uint4 v = reinterpret_cast<const uint4 *>(priv)[G::at1(q)];
+                                const uint4 d = reinterpret_cast<const uint4 *>(shared)[(G::kShared + priv_layer<L, LR, PK, E>(t)) * G::SPC + piece];
+                                x[kc] = uint4{v.x ^ d.x, v.y ^ d.y, v.z ^ d.z, v.w ^ d.w};
+                            }
+                        });
+                        static_for<0, KP3>([&](auto kc) {
+                            const uint32_t q = lane + 64u * decltype(kc)::value;
+                            if (q < PC * G::kP3) reinterpret_cast<uint4 *>(priv)[G::at1(q)] = x[kc];
+                        });
+                    }
+                    return;
+                }
+                static_for<0, KP3>([&](auto kc) {
+                    const uint32_t q = lane + 64u * decltype(kc)::value;
+                    if (q < PC * G::kP3) reinterpret_cast<uint4 *>(priv)[G::at1(q)] = v3[kc];
+                });
+            };
+            // B0: the FFT's layer-0 tables (phase 3's last layer), requested while the
+            // FFT's phase 2 runs, take their turn in the region before that layer
+            uint4 v4[KP0];
+            auto issue4 = [&](bool need) {
+                if constexpr (G::B0)
+                    static_for<0, KP0>([&](auto kc) {
+                        const uint32_t q = lane + 64u * decltype(kc)::value;
+                        const uint32_t qc = clamp_piece(q, PC * G::kL0);
+                        v4[kc] = l0_piece<L, LR, PK, E>(img_f, wave, need ? qc : qc % PC);
+                    });
+            };
+            auto write4 = [&]() {
+                if constexpr (G::B0)
+                    static_for<0, KP0>([&](auto kc) {
+                        const uint32_t q = lane + 64u * decltype(kc)::value;
+                        if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at0(q)] = v4[kc];
+                    });
+            };
+            // 2-element decodes: the reveal tables are requested just before the FFT's
+            // last remap (with phase 3's table writes), so they land while phase 3 runs
+            constexpr bool kPreReveal = DEC && E == 2 && kQuadGather;
+            RevealTabs<LR> rt;
+            auto pre3 = [&](bool alive) {
+                return [&, alive]() {
+                    write3();
+                    (void)alive;
+                    if constexpr (kPreReveal)
+                        if (alive) reveal_issue<L, LR, PK>(A, ri, rt, lane, wave);
+                };
+            };
+            if constexpr (SPLIT) {
+                // the wave's half: the highest wave bit in both placements
+                constexpr uint32_t kHalfWords = (G::n / 2) / 32;
+                uint32_t half_any = 0;
+                const uint32_t h = wave >> (L - 1 - G::IW);
+                for (uint32_t k = 0; k < kHalfWords; ++k) half_any |= K.received[h * kHalfWords + k];
+                // IFFT: a wave whose rows hold no received row skips phase 1 (its rows
+                // stay zero), a half without received rows skips phase 2
+                run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 1 : -1, PK>(ts, c, plane, lane, wave, issue3,
+                                                                             half_any != 0, live, write1);
+                RS_MSTAMP(5);
+                using SF = SeqOf<L, LR, true, PK>;
+                constexpr int NLF = num_layers(SF::v);
+                const bool out = out_wave;
+                const bool alive = out && wave_stores<L, LR, PK>(A, wave);
+                constexpr uint32_t kTopI = (G::n >> G::IW) - 2, kTopF = G::kShI + (G::n >> G::FLO) - 2;
+                split_top<L, LR>(c, plane, lds + G::words_dec, shared + kTopI * G::SW, shared + kTopF * G::SW, lane, wave,
+                                 A.out_half);
+                RS_MSTAMP(6);
+                issue4(alive);
+                // FFT below the top layer: only the half that holds restored rows
+                run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, PK>(ts, c, plane, lane, wave, pre3(alive),
+                                                                                  alive, out, write4);
+                if (!alive) return;
+            } else if constexpr (G::WB > 0) {
+                run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 1 : -1, PK>(ts, c, plane, lane, wave, issue3, true, live,
+                                                                       write1);
+                RS_MSTAMP(5);
+                using SF = SeqOf<L, LR, true, PK>;
+                constexpr int NLF = num_layers(SF::v);
+                const bool alive = !DEC || wave_stores<L, LR, PK>(A, wave);
+                issue4(alive);  // (waves that stop early all read one table: no branch around the loads)
+                if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
+                run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, PK>(ts, c, plane, lane, wave, pre3(alive), alive,
+                                                                            true, write4);
+                if (!alive) return;
+            } else {
+                static_assert(!G::B0, "one-segment plans keep every table in the region");
+                run_seq<L, LR, false, RS_MONO_LDS_PF, -1, PK>(ts, c, plane, lane, wave, NoHook{});
+                issue3();
+                if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
+                write3();
+                run_seq<L, LR, true, RS_MONO_LDS_PF, -1, PK>(ts, c, plane, lane, wave, NoHook{});
+            }
+            RS_MSTAMP(10);
+            store_col<L, LR, DEC, PK>(A, ri, 0, io, sb, c, lane, wave, kPreReveal && G::WB > 0 ? &rt : nullptr);
+            RS_MSTAMP(11);
+      };
+      if constexpr (MODE == kMonoDecode) {
+          if (io.bytes) staged(std::integral_constant<int, 1>{});
+          else staged(std::integral_constant<int, 0>{});
+      } else {
+          staged(std::integral_constant<int, -1>{});
+      }
     } else if constexpr (MODE == kMonoEncodeHigh) {
         // rate_high.rs:44-87: recovery = FFT_0(XOR_c IFFT_{c n + n}(chunk c))
         load_col<L, LR, false>(A, 0, io, sb, c, lane, wave);
@@ -1819,12 +1861,11 @@ hipError_t launch_ls(const MonoArgs &A, hipStream_t s) {
     // 2-element packs exist to spread a launch over more CUs: more than half the
     // CU's LDS keeps the dispatcher from doubling workgroups up on one CU
     if (E == 2 && lds <= 80 * 1024) lds = 84 * 1024;
-    static bool attr_set = false;  // benign race: idempotent attribute call
-    if (!attr_set && lds > 65536) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mono<L, LR, MODE, STAGED, BATCH, SPLIT, E>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    static std::atomic<uint64_t> attr_devs{0};  // devices whose attribute is set
+    if (lds > 65536) {
+        hipError_t e = lds_attr_once(
+            attr_devs, reinterpret_cast<const void *>(&k_mono<L, LR, MODE, STAGED, BATCH, SPLIT, E>), int(lds));
         if (e != hipSuccess) return e;
-        attr_set = true;
     }
     const uint32_t grid = 8u * A.packs_per_xcd;
     k_mono<L, LR, MODE, STAGED, BATCH, SPLIT, E>
