@@ -1513,13 +1513,13 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             // 1's, still in the region when phase 1 ran on real tables (live): the
             // same tables when IFFT and FFT share the skew offset (decodes,
             // rate_high.rs:213-245), else phase 1's XOR D_b (encodes, Stage::kD)
-    #ifndef RS_MONO_NO_REUSE
+#ifndef RS_MONO_NO_REUSE
             const bool same3 = A.ifft_img == A.fft_img;
             const bool reuse3 = live && (same3 || kDerive3);
-    #else
+#else
             const bool same3 = A.ifft_img == A.fft_img;
             const bool reuse3 = false;
-    #endif
+#endif
 
             // every global read is requested before any of them is waited for.
             // Decodes: eval_poly's inputs first.  Thread t's erased / received bits
@@ -1544,11 +1544,11 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             // no rows, no phase-1 tables and no scale tables (uniform branches: the
             // vector-memory issue rate of the ~330 load instructions of a 2^11-row
             // workgroup bounds the prologue, and 7 of 16 waves are not live at 1 %)
-    #ifndef RS_MONO_DEC_LOAD_ALL
+#ifndef RS_MONO_DEC_LOAD_ALL
             const bool skip = DEC && !live;
-    #else
+#else
             const bool skip = false;
-    #endif
+#endif
             uint32_t w[2 << LR] = {};
             uint32_t okm = 0;
             auto issue_rows = [&](auto bytes) {
@@ -1560,7 +1560,7 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             // layers above when layer 0 has read them (run_seq's hook)
             uint4 v0[KP0], v1[KP1], vs[KSH];
             auto issue_priv = [&]() {
-    #ifndef RS_MONO_SKIP_STAGE  // tools/mono_probe.hip ablation
+#ifndef RS_MONO_SKIP_STAGE  // tools/mono_probe.hip ablation
                 if constexpr (G::B0)
                     static_for<0, KP0>([&](auto kc) {
                         const uint32_t q = clamp_piece(lane + 64u * decltype(kc)::value, PC * G::kL0);
@@ -1570,11 +1570,11 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                     const uint32_t q = clamp_piece(lane + 64u * decltype(kc)::value, PC * G::kUp);
                     v1[kc] = priv_piece<L, LR, PK, E>(img_i, wave, live ? q : q % PC);
                 });
-    #endif
+#endif
             };
             // the shared region: every thread of the workgroup loads and writes pieces
             auto issue_shared = [&]() {
-    #ifndef RS_MONO_SKIP_STAGE
+#ifndef RS_MONO_SKIP_STAGE
                 if constexpr (kSh > 0)
                     static_for<0, KSH>([&](auto kc) {
                         const uint32_t q = clamp_piece(threadIdx.x + T * decltype(kc)::value, PC * kSh);
@@ -1586,16 +1586,16 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                             vs[kc] = ld_piece(src);
                         }
                     });
-    #endif
+#endif
             };
             // Decodes, order of the loads around eval_poly (inputs first, see above).
             // RS_MONO_DEC_ORDER 1: the shared tables, the live waves' rows and phase-1
             // tables, all in flight while eval_poly runs, then the scale gathers;
             // 2: rows, eval_poly, gathers, then the tables; 3: shared tables and rows,
             // eval_poly, gathers, phase-1 tables
-    #ifndef RS_MONO_DEC_ORDER
-    #define RS_MONO_DEC_ORDER 1
-    #endif
+#ifndef RS_MONO_DEC_ORDER
+#define RS_MONO_DEC_ORDER 1
+#endif
             constexpr int kOrder = RS_MONO_DEC_ORDER;
             // 4: the shared tables only, eval_poly, then rows, gathers, phase-1 tables
             constexpr bool kShFirst = kOrder != 2, kPrivFirst = kOrder == 1, kRowsFirst = kOrder != 4;
@@ -1607,13 +1607,13 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             // path and hold live waves until their rows land -- so each path gets its
             // own copy of eval_poly, on straight-line code after its loads
             auto eval = [&]() {
-    #ifndef RS_MONO_SKIP_EVAL  // tools/mono_probe.hip ablation
+#ifndef RS_MONO_SKIP_EVAL  // tools/mono_probe.hip ablation
                 col_eval_poly<L>(A, ebits, rbits, lwv, plane, rinfo);
-    #else
+#else
                 rinfo[2 * threadIdx.x] = ebits & 1u ? 0x10000u : lwv & 0xFFFFu;
                 rinfo[2 * threadIdx.x + 1] = ebits & 2u ? 0x10000u : lwv >> 16;
                 __syncthreads();
-    #endif
+#endif
             };
             using kIO = std::integral_constant<int, kBytesIO>;
             if constexpr (!DEC) {
@@ -1648,14 +1648,14 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             }
             RS_MSTAMP(13);
             auto write1 = [&]() {
-    #ifndef RS_MONO_SKIP_STAGE
+#ifndef RS_MONO_SKIP_STAGE
                 static_for<0, KP1>([&](auto kc) {
                     const uint32_t q = lane + 64u * decltype(kc)::value;
                     if (q < PC * G::kUp) reinterpret_cast<uint4 *>(priv)[G::at1(q)] = v1[kc];
                 });
-    #endif
+#endif
             };
-    #ifndef RS_MONO_SKIP_STAGE
+#ifndef RS_MONO_SKIP_STAGE
             if (!skip) {  // (a skipping wave's region is written by phase 3's tables before use)
                 if constexpr (G::B0)
                     static_for<0, KP0>([&](auto kc) {
@@ -1669,7 +1669,7 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 const uint32_t q = threadIdx.x + T * decltype(kc)::value;
                 if (q < PC * kSh) reinterpret_cast<uint4 *>(shared)[G::atS(q)] = vs[kc];
             });
-    #endif
+#endif
             finish_col<L, LR, DEC>(w, okm, &st, c, lane, io);
             RS_MSTAMP(1);
             const LdsTabs<L, LR, PK, E> ts{priv, shared, img_i, img_f};
