@@ -136,6 +136,45 @@ def test_decode_device_matches_oracle(torch, rs, rate, N, M, S, loss):
     assert np.all(got[~miss] == 0x33), "present rows of the output must not be written"
 
 
+# decodes of at most 64 work rows: one pass that evaluates eval_poly itself
+# (rs_kernels.hip pass_eval_poly); (rate, N, M): work rows 2..64, both rates,
+# the LowRate end < n and the HighRate recovery padding
+SMALL_DEC = [("high", 1, 1), ("low", 1, 1), ("high", 3, 5), ("low", 5, 3), ("high", 2, 30), ("low", 30, 2),
+             ("high", 32, 32), ("low", 32, 32), ("high", 31, 17), ("low", 17, 31), ("high", 40, 16),
+             ("low", 16, 40), ("high", 1, 32), ("low", 32, 1)]
+
+
+def _work_rows(rate, N, M):
+    chunk = 1 << max(0, ((M if rate == "high" else N) - 1).bit_length())
+    end = chunk + (N if rate == "high" else M)
+    return 1 << (end - 1).bit_length()
+
+
+@pytest.mark.parametrize("rate,N,M", SMALL_DEC)
+@pytest.mark.parametrize("S", [64, 1024, 130])
+def test_small_decode_is_one_fused_launch(torch, rs, rate, N, M, S):
+    assert _work_rows(rate, N, M) <= 64
+    rng = np.random.default_rng(N * 97 + M + S)
+    orig = O.generate_original(N, S, (N + M + S) & 0xFF)
+    rec = O.encode(rate, orig, M)
+    for trial in range(3):
+        L = int(rng.integers(1, min(N, M) + 1))
+        op = np.ones(N, np.uint8)
+        op[rng.choice(N, L, replace=False)] = 0
+        rp = np.zeros(M, np.uint8)
+        rp[rng.choice(M, L, replace=False)] = 1
+        want = O.decode(rate, orig, op, rec, rp)
+        rs.profile_enable(True)
+        try:
+            got = gpu_decode(torch, rs, rate, orig, op, rec, rp)
+            names = [r[0] for r in rs.profile_collect()]
+        finally:
+            rs.profile_enable(False)
+        miss = op == 0
+        assert np.array_equal(got[miss], orig[miss]) and np.array_equal(got[miss], want[miss]), (trial, L)
+        assert len(names) == 1 and names[0].startswith("k_pass<") and names[0].endswith(", 435>"), names
+
+
 # ---------------------------------------------------------------------------
 # the reference's golden vectors through the drop-in object API
 

@@ -1,0 +1,121 @@
+"""Checks of the built gfx950 code object (CPU: disassembly, no GPU).
+
+Two kernels wait for memory by counts the compiler does not derive itself:
+
+* k_stream (rs_kernels.hip): its rows arrive by LDS-DMA (inline asm, so hipcc
+  does not see them) and it waits for a block's DMA with s_waitcnt vmcnt(N),
+  N = the store instructions issued after that DMA.  That is exact only if
+  every DMA and store instruction is issued whenever its site runs: the DMAs
+  come in asm statements of 8 global_load_lds_dword, the stores in one of 16
+  global_store_dword, and no branch may jump over part of one.
+* the staged decode column kernel (rs_mono.hip) loads lw_fold first and has
+  the compiler place the wait for it at its first use, after eval_poly's first
+  transform; on the path that issues the row and table loads that wait must
+  leave them in flight (vmcnt(13) in the headline decode: 1 shared-table load,
+  4 row loads, 8 phase-1 table loads issued after lw_fold).  A smaller count
+  would still be correct but would hold eval_poly until the rows land.
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "reed-solomon-simd_amd", "lib", "librs_mi355x.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def _disassemble(tmp_path_factory):
+    tools = [os.path.join(LLVM, t) for t in ("llvm-objcopy", "clang-offload-bundler", "llvm-objdump")]
+    if not all(os.path.exists(t) for t in tools) or not os.path.exists(LIB):
+        pytest.skip("ROCm LLVM tools or the built library missing")
+    d = tmp_path_factory.mktemp("isa")
+    fat = str(d / "fat")
+    subprocess.run([tools[0], "-O", "binary", "--only-section=.hip_fatbin", LIB, fat], check=True)
+    # the section holds one offload bundle per translation unit, each opening with the magic
+    data = open(fat, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+    out = ""
+    for k, a in enumerate(starts):
+        part, co = str(d / ("b%d" % k)), str(d / ("co%d" % k))
+        with open(part, "wb") as f:
+            f.write(data[a:starts[k + 1] if k + 1 < len(starts) else len(data)])
+        subprocess.run([tools[1], "--unbundle", "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
+                        "--input=" + part, "--output=" + co], check=True)
+        out += subprocess.run([tools[2], "-d", co], check=True, capture_output=True, text=True).stdout
+    # per kernel: [(address, instruction, branch target or None)]
+    kernels, name, body, base = {}, None, [], 0
+    for line in out.splitlines():
+        m = re.match(r"^([0-9a-f]+) <(\S+)>:$", line)
+        if m:
+            if name:
+                kernels[name] = body
+            name, body, base = m.group(2), [], int(m.group(1), 16)
+        elif name and line.startswith("\t"):
+            ins, _, comment = line.partition("//")
+            a = re.match(r"\s*([0-9A-Fa-f]+):", comment)
+            t = re.search(r"<\S+\+0x([0-9a-f]+)>", comment)
+            body.append((int(a.group(1), 16) if a else None, ins.strip(),
+                         base + int(t.group(1), 16) if t else None))
+    if name:
+        kernels[name] = body
+    return kernels
+
+
+@pytest.fixture(scope="module")
+def kernels(tmp_path_factory):
+    return _disassemble(tmp_path_factory)
+
+
+def _partly_skipped(body, site):
+    """Whether some forward branch jumps over part (not all) of a site's instructions."""
+    addrs = [body[j][0] for j in site]
+    for a, ins, t in body:
+        if t is not None and a is not None and (ins.startswith("s_cbranch") or ins.startswith("s_branch")):
+            n = sum(a < x < t for x in addrs)
+            if 0 < n < len(addrs):
+                return True
+    return False
+
+
+def test_stream_kernels_issue_every_counted_instruction(kernels):
+    stream = {k: v for k, v in kernels.items() if "8k_stream" in k}
+    assert len(stream) >= 15, sorted(stream)
+    for name, body in stream.items():
+        dma = [i for i, (_, ins, _) in enumerate(body) if ins.startswith("global_load_lds_dword")]
+        stores = [i for i, (_, ins, _) in enumerate(body) if ins.startswith("global_store_dword")]
+        # two DMA sites (before the loop, in it) of two 8-instruction statements, one 16-store statement
+        assert len(dma) == 32 and len(stores) == 16, (name, len(dma), len(stores))
+        groups = [dma[g:g + 8] for g in range(0, 32, 8)]
+        for grp in groups:  # one asm statement: nothing but M0 steps between its DMAs
+            between = [body[j][1] for j in range(grp[0], grp[-1] + 1) if j not in grp]
+            assert all(b.startswith("s_add_u32 m0") or b.startswith("s_nop") for b in between), (name, between)
+        assert stores == list(range(stores[0], stores[0] + 16)), name
+        # no branch skips part of a group: each instruction is issued whenever its statement runs
+        for grp in groups + [stores]:
+            assert not _partly_skipped(body, grp), (name, grp[0])
+        # the block waits: vmcnt(16) (the last block's stores outstanding) and vmcnt(0)
+        waits = {int(m.group(1)) for _, ins, _ in body for m in [re.match(r"s_waitcnt vmcnt\((\d+)\)$", ins)] if m}
+        assert 16 in waits and 0 in waits, (name, waits)
+
+
+def test_headline_decode_leaves_row_loads_in_flight(kernels):
+    name = next((k for k in kernels if "k_monoILi11ELi1ELi2ELb1ELb0ELb1ELi2E" in k), None)
+    assert name, "headline decode kernel k_mono<11, 1, 2, true, false, true, 2> not found"
+    body = [ins for _, ins, _ in kernels[name]]
+    first = next(i for i, ins in enumerate(body) if ins.startswith("global_load_dword "))
+    reg = body[first].split()[1].rstrip(",")  # the lw_fold destination
+    waits = []
+    for i in range(first + 1, len(body)):
+        ins = body[i]
+        if ins.startswith("v_mul") and re.search(r"\b%s\b" % re.escape(reg), ins):  # x * lw_fold
+            # the wait in force at this read of lw_fold: the last vmcnt before it
+            for j in range(i - 1, first, -1):
+                m = re.match(r"s_waitcnt vmcnt\((\d+)\)", body[j])
+                if m:
+                    waits.append(int(m.group(1)))
+                    break
+    # skip path (the shared-table load only after it: 1), live path (13 loads after it)
+    assert 13 in waits, waits

@@ -54,7 +54,12 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&orig, bytes));
     CK(hipMalloc(&W, bytes));
     CK(hipMalloc(&rec, bytes));
-    CK(hipMemset(orig, 0x5A, bytes));
+    {  // pseudo-random originals (a constant fill would hide errors)
+        std::vector<uint8_t> h(bytes);
+        uint64_t x = 0x9E3779B97F4A7C15ull;
+        for (size_t i = 0; i < bytes; ++i) x ^= x << 13, x ^= x >> 7, x ^= x << 17, h[i] = uint8_t(x);
+        CK(hipMemcpy(orig, h.data(), bytes, hipMemcpyHostToDevice));
+    }
     CK(hipMemset(W, 0, bytes));
     uint32_t L = 0;
     while ((1u << L) < n) ++L;
@@ -85,15 +90,53 @@ int main(int argc, char **argv) {
     const double gb = 2.0 * double(bytes) / 1e9;
     const size_t n16 = bytes / 16;
     const double tc = time_us([&] { k_copy<<<8192, 256>>>((const uint4 *)orig, (uint4 *)rec, n16); }, iters);
-    printf("copy 2x%zu B  %9.1f us  %6.2f TB/s\n", bytes, tc, gb / tc * 1e-3 * 1e3);
-    auto run = [&](const char *name, int K, int flags, const rs::PassArgs &X) {
-        const double t = time_us([&] { CK(rs::launch_pass(K, flags, X, 0)); }, iters);
-        printf("%-10s K=%d  %9.1f us  %6.2f TB/s  (%s)\n", name, K, t, gb / t * 1e-3 * 1e3, rs::launch_name_buf());
-        return t;
-    };
-    const double t1 = run("ifft", K0, rs::kIfft, P);
-    const double t2 = run("ifft+fft", K1, rs::kIfft | rs::kFft, Q);
-    const double t3 = run("fft", K0, rs::kFft, F);
-    printf("encode (3 passes) %9.1f us  %7.1f GiB/s\n", t1 + t2 + t3, 2.0 * bytes / (t1 + t2 + t3) * 1e6 / (1u << 30));
+    printf("copy 2x%zu B  %9.1f us  %6.2f TB/s\n", bytes, tc, gb / tc * 1e3);
+    // the streaming pass (k_stream) beside the one-block-per-workgroup pass (k_pass)
+    uint8_t *zeros;
+    CK(hipMalloc(&zeros, 512));
+    CK(hipMemset(zeros, 0, 512));
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    for (rs::PassArgs *X : {&P, &Q, &F}) X->zeros = zeros, X->junk = zeros + 256, X->cus = uint32_t(cus);
+    for (int stream = 0; stream < 2; ++stream) {
+        auto run = [&](const char *name, int K, int flags, const rs::PassArgs &X) {
+            const bool st = stream && rs::stream_supported(K, flags, X);
+            const double t = time_us([&] { CK(st ? rs::launch_stream(K, flags, X, X.cus, 0) : rs::launch_pass(K, flags, X, 0)); }, iters);
+            printf("%-10s K=%d  %9.1f us  %6.2f TB/s  (%s)\n", name, K, t, gb / t * 1e3, rs::launch_name_buf());
+            return t;
+        };
+        const double t1 = run("ifft", K0, rs::kIfft, P);
+        const double t2 = run("ifft+fft", K1, rs::kIfft | rs::kFft, Q);
+        const double t3 = run("fft", K0, rs::kFft, F);
+        printf("encode (3 passes%s) %9.1f us  %7.1f GiB/s\n", stream ? ", streaming" : "", t1 + t2 + t3,
+               2.0 * bytes / (t1 + t2 + t3) * 1e6 / (1u << 30));
+    }
+    // parity of the streaming passes against k_pass on this shape (whole recovery matrix)
+    {
+        uint8_t *rec2;
+        CK(hipMalloc(&rec2, bytes));
+        CK(hipMemset(W, 0, bytes));
+        CK(rs::launch_pass(K0, rs::kIfft, P, 0));
+        CK(rs::launch_pass(K1, rs::kIfft | rs::kFft, Q, 0));
+        CK(rs::launch_pass(K0, rs::kFft, F, 0));
+        CK(hipMemcpy(rec2, rec, bytes, hipMemcpyDeviceToDevice));
+        CK(hipMemset(W, 0, bytes));
+        CK(hipMemset(rec, 0, bytes));
+        auto go = [&](int K, int fl, const rs::PassArgs &X) {
+            CK(rs::stream_supported(K, fl, X) ? rs::launch_stream(K, fl, X, X.cus, 0) : rs::launch_pass(K, fl, X, 0));
+        };
+        go(K0, rs::kIfft, P);
+        go(K1, rs::kIfft | rs::kFft, Q);
+        go(K0, rs::kFft, F);
+        CK(hipDeviceSynchronize());
+        std::vector<uint8_t> a(bytes), b(bytes);
+        CK(hipMemcpy(a.data(), rec, bytes, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(b.data(), rec2, bytes, hipMemcpyDeviceToHost));
+        uint64_t h = 0xcbf29ce484222325ull;  // FNV-1a of the k_pass recovery rows (compare across -D variants)
+        for (uint8_t v : b) h = (h ^ v) * 0x100000001b3ull;
+        printf("k_pass recovery hash %016llx\n", (unsigned long long)h);
+        printf("streaming vs k_pass recovery rows: %s\n", a == b ? "identical" : "DIFFER");
+        if (a != b) return 1;
+    }
     return 0;
 }

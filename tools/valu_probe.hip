@@ -18,8 +18,14 @@ __global__ void k_rate(uint64_t *out, int iters) {
             } else if constexpr (OP == 1) {
                 asm volatile("v_lshrrev_b32 %0, 3, %0\n v_lshrrev_b32 %1, 3, %1\n v_lshrrev_b32 %2, 3, %2\n v_lshrrev_b32 %3, 3, %3"
                              : "+v"(e), "+v"(f), "+v"(g), "+v"(h));
-            } else {
+            } else if constexpr (OP == 2) {
                 asm volatile("v_perm_b32 %0, %1, %2, %3\n v_perm_b32 %1, %2, %3, %0\n v_perm_b32 %2, %3, %0, %1\n v_perm_b32 %3, %0, %1, %2"
+                             : "+v"(e), "+v"(f), "+v"(g), "+v"(h));
+            } else if constexpr (OP == 3) {
+                asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96\n v_bitop3_b32 %1, %2, %3, %0 bitop3:0x96\n v_bitop3_b32 %2, %3, %0, %1 bitop3:0x96\n v_bitop3_b32 %3, %0, %1, %2 bitop3:0x96"
+                             : "+v"(e), "+v"(f), "+v"(g), "+v"(h));
+            } else {  // a v_perm / v_bitop3 / v_and mix, as in a butterfly
+                asm volatile("v_perm_b32 %0, %1, %2, %3\n v_bitop3_b32 %1, %2, %3, %0 bitop3:0x96\n v_and_b32 %2, %3, %0\n v_perm_b32 %3, %0, %1, %2"
                              : "+v"(e), "+v"(f), "+v"(g), "+v"(h));
             }
         }
@@ -33,13 +39,15 @@ int main() {
     uint64_t *d;
     (void)hipMalloc(&d, 8 * 2048);
     const int iters = 1000;
-    const char *names[3] = {"v_lshrrev_b64", "v_lshrrev_b32", "v_perm_b32"};
-    for (int waves : {1, 4, 16}) {
-        for (int op = 0; op < 3; ++op) {
+    const char *names[5] = {"v_lshrrev_b64", "v_lshrrev_b32", "v_perm_b32", "v_bitop3_b32", "perm/bitop3/and"};
+    for (int waves : {1, 4, 8, 16}) {
+        for (int op = 0; op < 5; ++op) {
             auto launch = [&] {
                 if (op == 0) k_rate<0><<<1, 64 * waves>>>(d, iters);
                 else if (op == 1) k_rate<1><<<1, 64 * waves>>>(d, iters);
-                else k_rate<2><<<1, 64 * waves>>>(d, iters);
+                else if (op == 2) k_rate<2><<<1, 64 * waves>>>(d, iters);
+                else if (op == 3) k_rate<3><<<1, 64 * waves>>>(d, iters);
+                else k_rate<4><<<1, 64 * waves>>>(d, iters);
             };
             launch();
             (void)hipDeviceSynchronize();
