@@ -329,16 +329,6 @@ rs_status rs_check_device(rs_context *ctx);
  * included.  A/B and tests; results are identical in every mode. */
 rs_status rs_mono_enable(rs_context *ctx, int enable);
 
-/* ---- streaming pass control (engine tuning, not a reference item) ----
- * Passes over large matrices (at least 4096 blocks of 2^K rows x one column
- * slice) of the encode transforms run as one launch of persistent 1024-thread
- * workgroups, one per CU, that load the next block's rows by LDS-DMA while the
- * current one computes (DESIGN.md "Streaming pass").  mode 0: never (also
- * RS_MI355X_STREAM=0 at context creation); 1 (default): from 4096 blocks; 2:
- * wherever the pass's shape is supported (tests).  Results are identical in
- * every mode. */
-rs_status rs_stream_enable(rs_context *ctx, int mode);
-
 /* ---- GF(2^16) tables (src/engine/tables.rs), host copies ---- */
 const uint16_t *rs_table_exp(void);       /* 65536 */
 const uint16_t *rs_table_log(void);       /* 65536 */

@@ -201,10 +201,6 @@ struct rs_context {
     uint32_t e2_max_packs = 192;
     bool e2_encode = false;
     int chunk_par = -1;           // RS_MI355X_CHUNK_PARALLEL: -1 by pack count (chunk_parallel), 0 / 1 forced
-    // streaming pass kernel (rs_stream_enable): 0 off, 1 passes of >= 4096 blocks, 2 wherever supported
-    int stream = 0;
-    uint32_t cus = 0;             // compute units of the device
-    uint8_t *d_zeros = nullptr;   // 256 zero bytes + 256 junk bytes (streaming pass)
     uint32_t *d_lut2 = nullptr;   // perm2_by_log: the 2-element form of d_lut
     std::mutex img_mu;            // guards d_img, d_img2
     uint32_t *d_img[13] = {};     // column-kernel twiddle images per L (built at context creation)
@@ -385,12 +381,6 @@ rs::PassArgs base_args(rs_context *ctx, const Geom &g, uint32_t n) {
     A.tw = ctx->d_tw;
     A.lut = ctx->d_lut;
     A.fmt = g.fmt;
-    if (ctx->stream) {
-        A.zeros = ctx->d_zeros;
-        A.junk = ctx->d_zeros + 256;
-        A.cus = ctx->cus;
-        A.stream_min_blocks = ctx->stream == 2 ? 1u : 4096u;
-    }
     return A;
 }
 
@@ -448,9 +438,7 @@ void launch(int K, int flags, rs::PassArgs A, uint32_t nsets, uint32_t a, hipStr
     A.a = a;
     hipEvent_t ev = nullptr;
     if (t_prof_ctx) prof_begin(s, &ev);
-    // large matrices: the streaming form (rs_kernels.hip k_stream) where it applies
-    if (A.cus && rs::stream_supported(K, flags, A)) check(rs::launch_stream(K, flags, A, A.cus, s));
-    else check(rs::launch_pass(K, flags, A, s));
+    check(rs::launch_pass(K, flags, A, s));
     if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), pass_bytes(K, A, dec_rd, dec_wr));
 }
 
@@ -1261,13 +1249,6 @@ rs_status rs_context_create(int device, rs_context **out) {
         check(hipMemcpy(ctx->d_tw, T.perm_by_skew.data(), T.perm_by_skew.size() * 4, hipMemcpyHostToDevice));
         check(hipMemcpy(ctx->d_lut, T.perm_by_log.data(), T.perm_by_log.size() * 4, hipMemcpyHostToDevice));
         check(hipMemcpy(ctx->d_lwfold, T.lw_fold.data(), T.lw_fold.size() * 2, hipMemcpyHostToDevice));
-        check(hipMalloc(&ctx->d_zeros, 512));
-        check(hipMemset(ctx->d_zeros, 0, 512));
-        int cus = 0;
-        check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-        ctx->cus = uint32_t(cus);
-        const char *sm = getenv("RS_MI355X_STREAM");  // (A/B) "0" / "1" / "2" as rs_stream_enable
-        if (sm && sm[0] >= '0' && sm[0] <= '2' && !sm[1]) ctx->stream = sm[0] - '0';
         check(hipMalloc(&ctx->d_lut2, T.perm2_by_log.size() * 4));
         check(hipMemcpy(ctx->d_lut2, T.perm2_by_log.data(), T.perm2_by_log.size() * 4, hipMemcpyHostToDevice));
         ctx->lw0 = T.log_walsh[0];
@@ -1306,7 +1287,6 @@ void rs_context_destroy(rs_context *ctx) {
     if (ctx->d_tw) (void)hipFree(ctx->d_tw);
     if (ctx->d_lut) (void)hipFree(ctx->d_lut);
     if (ctx->d_lut2) (void)hipFree(ctx->d_lut2);
-    if (ctx->d_zeros) (void)hipFree(ctx->d_zeros);
     for (uint32_t *p : ctx->d_img2)
         if (p) (void)hipFree(p);
     if (ctx->d_lwfold_base) (void)hipFree(ctx->d_lwfold_base);
@@ -2104,13 +2084,6 @@ rs_status rs_mono_enable(rs_context *ctx, int enable) {
     // + 8: 4-element packs only; + 16: 2-element packs wherever the staged kernel runs
     ctx->e2_max_packs = (enable & 8) ? 0u : (enable & 16) ? 0xFFFFFFFFu : 192u;
     ctx->e2_encode = (enable & 16) != 0;
-    return RS_OK;
-}
-
-rs_status rs_stream_enable(rs_context *ctx, int mode) {
-    if (!ctx || mode < 0 || mode > 2) return RS_ERR_INVALID_ARGUMENT;
-    std::lock_guard<std::mutex> lock(ctx->mu);
-    ctx->stream = mode;
     return RS_OK;
 }
 

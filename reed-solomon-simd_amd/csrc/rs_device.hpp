@@ -151,13 +151,6 @@ struct PassArgs {
     uint64_t zero_in[4] = {0, 0, 0, 0};
     uint64_t keep_out[4] = {~0ull, ~0ull, ~0ull, ~0ull};
 
-    // ---- streaming pass (launch_stream): 256 bytes of zeros a DMA of a row
-    // outside the matrices reads, and a junk line stores of such rows write
-    const uint8_t *zeros = nullptr;
-    uint8_t *junk = nullptr;
-    uint32_t cus = 0;  // host side: the device's compute units (0: no streaming pass)
-    uint32_t stream_min_blocks = 4096;  // host side: blocks (set x slice) a pass needs to stream
-
     // ---- single-pass decodes of at most kPassEvalRows work rows (fused_eval = 1):
     // every workgroup evaluates eval_poly itself (as k_eval_poly, rs_eval.hip)
     // into its LDS row info instead of reading rowinfo -- one launch, not two
@@ -182,11 +175,6 @@ enum PassFlags {
 
 // Launch one pass on `stream`.  K = log2(rows per set).
 hipError_t launch_pass(int K, int flags, const PassArgs &args, hipStream_t stream);
-// The streaming form of one pass (k_stream: persistent 1024-thread workgroups,
-// the next block's rows by LDS-DMA while the current one computes), for the
-// shapes stream_supported() accepts; `cus` = the device's compute units.
-bool stream_supported(int K, int flags, const PassArgs &args);
-hipError_t launch_stream(int K, int flags, const PassArgs &args, uint32_t cus, hipStream_t stream);
 
 // Name of the kernel the last launch_pass / launch_mono call of this thread
 // launched, in rocprofv3's short form ("k_pass<8, 3, 4, 1>"): the profiler's

@@ -431,15 +431,6 @@ __device__ __forceinline__ void layer(const Ctx &c, const uint32_t *tab, uint32_
     });
 }
 
-// Workgroup barrier.  RAW (the streaming pass, k_stream): s_barrier after this
-// wave's LDS accesses are done, without the vmcnt(0) a __syncthreads() emits
-// while an LDS-DMA is in flight -- that would drain the next block's rows.
-template <bool RAW>
-__device__ __forceinline__ void block_sync() {
-    if constexpr (RAW) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else __syncthreads();
-}
-
 // 2x2 transpose between lane rows 16 (LANE_BIT 4) or 32 (LANE_BIT 5) apart:
 // the lane with lane bit clear keeps a and takes its partner's a as b, the
 // partner keeps b and takes the a-lane's b as a (v_permlane{16,32}_swap).
@@ -490,30 +481,6 @@ __device__ __forceinline__ void exchange(const Ctx &c, uint32_t *plane, uint32_t
         lo[i] = plane[x];
         hi[i] = plane[kPlane + x];
     });
-}
-
-// The same through a one-plane region, the low words and then the high words,
-// with raw barriers (k_stream: an LDS-DMA is in flight; block_sync)
-template <int K, int LR, int SPL, int FROM, int TO>
-__device__ __forceinline__ void exchange_half(const Ctx &c, uint32_t *plane, uint32_t (&lo)[1 << LR],
-                                              uint32_t (&hi)[1 << LR]) {
-    using P = Pass<K, LR, SPL>;
-    if constexpr (FROM != TO) {
-        auto one = [&](uint32_t (&v)[1 << LR]) {
-            block_sync<true>();
-            static_for<0, P::R>([&](auto ic) {
-                constexpr int i = decltype(ic)::value;
-                plane[P::template lrow<FROM>(c.g, i) * P::SP + c.p] = v[i];
-            });
-            block_sync<true>();
-            static_for<0, P::R>([&](auto ic) {
-                constexpr int i = decltype(ic)::value;
-                v[i] = plane[P::template lrow<TO>(c.g, i) * P::SP + c.p];
-            });
-        };
-        one(lo);
-        one(hi);
-    }
 }
 
 // Formal derivative restricted to the set's local bits:
@@ -605,113 +572,26 @@ __device__ __forceinline__ void apply_layer(const LayerTabs<LR> &T, uint32_t (&l
     });
 }
 
-// The butterfly groups of a transform in order (layer n, group gc of the
-// lane's register groups of that layer): the unit the wide shapes run one
-// at a time.
-template <int K, int LR, int SPL, bool IFFT>
-struct GroupSeq {
-    using P = Pass<K, LR, SPL>;
-    static constexpr int bit(int n) { return IFFT ? n : K - 1 - n; }
-    static constexpr int rbit(int n) { return bit(n) - P::start(P::phase_of(bit(n))); }
-    static constexpr int groups(int n) { return P::R >> (rbit(n) + 1); }
-    static constexpr int total() {
-        int s = 0;
-        for (int n = 0; n < K; ++n) s += groups(n);
-        return s;
-    }
-    static constexpr int layer_of(int it) {
-        for (int n = 0; n < K; ++n) {
-            if (it < groups(n)) return n;
-            it -= groups(n);
-        }
-        return K;
-    }
-    static constexpr int group_of(int it) {
-        for (int n = 0; n < K; ++n) {
-            if (it < groups(n)) return it;
-            it -= groups(n);
-        }
-        return 0;
-    }
-};
-
-// Wide shapes: one butterfly group at a time (a chain through `dep`), with
-// the NEXT group's table read from LDS while this group computes -- two
-// tables live, and the LDS latency off the chain.
-template <int K, int LR, int SPL, bool IFFT, int XM>
-__device__ __forceinline__ void transform_serial(const Ctx &c, uint32_t *plane, const uint32_t *tab,
-                                                 uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
-    using P = Pass<K, LR, SPL>;
-    using Q = GroupSeq<K, LR, SPL, IFFT>;
-    constexpr int kItems = Q::total();
-    uint32_t T[2][20];
-    uint32_t dep = 0;
-    auto fetch = [&](auto itc, uint32_t (&t)[20]) {
-        constexpr int it = decltype(itc)::value;
-        constexpr int n = Q::layer_of(it), b = Q::bit(n), ph = P::phase_of(b);
-        uint32_t off = tw_slot<K>(b, P::template lrow<ph>(c.g, Q::group_of(it) << (Q::rbit(n) + 1))) * 20u;
-        if constexpr (P::kUniform) asm volatile("" : "+s"(off) : "v"(dep));
-        else asm volatile("" : "+v"(off) : "v"(dep));
-        const uint4 *t4 = reinterpret_cast<const uint4 *>(tab + off);
-#pragma unroll
-        for (int q = 0; q < 5; ++q) {
-            const uint4 v = t4[q];
-            t[4 * q] = v.x, t[4 * q + 1] = v.y, t[4 * q + 2] = v.z, t[4 * q + 3] = v.w;
-        }
-    };
-    fetch(std::integral_constant<int, 0>{}, T[0]);
-    static_for<0, kItems>([&](auto itc) {
-        constexpr int it = decltype(itc)::value;
-        constexpr int n = Q::layer_of(it), gc = Q::group_of(it), b = Q::bit(n), ph = P::phase_of(b);
-        constexpr int RB = Q::rbit(n);
-        if constexpr (gc == 0 && n > 0 && P::phase_of(Q::bit(n - 1)) != ph) {
-            constexpr int from = P::phase_of(Q::bit(n - 1));
-            if constexpr (XM == 2) exchange_half<K, LR, SPL, from, ph>(c, plane, lo, hi);
-            else exchange<K, LR, SPL, from, ph>(c, plane, lo, hi);
-        }
-        if constexpr (it + 1 < kItems) fetch(std::integral_constant<int, it + 1>{}, T[(it + 1) & 1]);
-        constexpr int i0 = gc << (RB + 1);
-        static_for<0, (1 << RB)>([&](auto lc) {
-            constexpr int i = i0 | decltype(lc)::value;
-            constexpr int i2 = i | (1 << RB);
-            asm volatile("" : "+v"(lo[i]), "+v"(hi[i]), "+v"(lo[i2]), "+v"(hi[i2]) : "v"(dep));
-            if constexpr (IFFT) ifft_bfly(lo[i], hi[i], lo[i2], hi[i2], T[it & 1]);
-            else fft_bfly(lo[i], hi[i], lo[i2], hi[i2], T[it & 1]);
-            dep = lo[i];
-        });
-    });
-}
-
-#ifndef RS_SERIAL_PIPE
-#define RS_SERIAL_PIPE 0
-#endif
-
 // IFFT: bits ascending, starting in phase 0, ending in phase NPH-1.
 // FFT: bits descending, starting in phase NPH-1, ending in phase 0.
 // Narrow shapes (<= 4 rows per lane) read layer n+1's tables into registers
 // while layer n runs, so the LDS latency hides behind the butterflies and
 // the phase exchanges; wide shapes read one table at a time (registers).
-// XM: exchange form -- 0: __syncthreads around a two-plane exchange (k_pass);
-// 2: raw barriers, one plane at a time through a one-plane region (k_stream)
-template <int K, int LR, int SPL, bool IFFT, int XM = 0>
+template <int K, int LR, int SPL, bool IFFT>
 __device__ __forceinline__ void transform(const Ctx &c, uint32_t *plane, const uint32_t *tab,
                                           uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
     using P = Pass<K, LR, SPL>;
 #ifdef RS_PROBE_SKIP_XFORM  // tools/pass_probe.hip: time a pass without its layers
     return;
 #endif
-    if constexpr (P::kSerial && K > 0 && RS_SERIAL_PIPE) {
-        transform_serial<K, LR, SPL, IFFT, XM>(c, plane, tab, lo, hi);
-    } else if constexpr (P::kSerial || K == 0) {
+    if constexpr (P::kSerial || K == 0) {
         static_for<0, K>([&](auto bc) {
             constexpr int n = decltype(bc)::value;
             constexpr int b = IFFT ? n : K - 1 - n;
             constexpr int prev = IFFT ? b - 1 : b + 1;
             constexpr int ph = P::phase_of(b);
-            if constexpr (n > 0 && P::phase_of(prev) != ph) {
-                if constexpr (XM == 2) exchange_half<K, LR, SPL, P::phase_of(prev), ph>(c, plane, lo, hi);
-                else exchange<K, LR, SPL, P::phase_of(prev), ph>(c, plane, lo, hi);
-            }
+            if constexpr (n > 0 && P::phase_of(prev) != ph)
+                exchange<K, LR, SPL, P::phase_of(prev), ph>(c, plane, lo, hi);
             layer<K, LR, SPL, ph, b, IFFT>(c, tab, lo, hi);
         });
     } else {
@@ -902,270 +782,6 @@ __global__ void __launch_bounds__(1 << (K - LR + SPL), (pass_waves_per_eu<LR, FL
     pass_body<K, LR, SPL, FLAGS>(A, blockIdx.x, blockIdx.y, lds);
 }
 
-// -------------------------------------------------------------------------
-// Streaming pass (k_stream).  The one-block-per-workgroup pass takes about the
-// sum of its row I/O and its butterflies (config 5's fused
-// pass 1.74 ms = row I/O 0.91 + staging 0.21 + layers 0.54): the loads of a
-// workgroup's block and its layers do not overlap.  Here persistent
-// workgroups, two per CU, each walk a run of consecutive blocks (set * slices +
-// slice: the slices of a set share their twiddle tables, staged once per set).
-// A block's rows arrive by LDS-DMA (global_load_lds_dword, no VGPRs) into the
-// workgroup's row buffer while the previous block computes; the exchanges go
-// through a one-plane region, low words then high words (exchange_half), so
-// two workgroups' buffers, planes and tables fit a CU's LDS and one's barriers
-// are covered by the other's work.
-template <int K>
-struct Stream {
-    static constexpr int LR = 3, NT = 512, NW = NT / 64;
-    static constexpr int SPL = 12 - K;  // 2^(K - 3) row groups x 2^SPL packs = 512 threads
-    using P = Pass<K, LR, SPL>;
-    static constexpr uint32_t SP = 1u << SPL;
-    static constexpr uint32_t kPlane = SP << K;       // words of one plane of a block (4096)
-    static constexpr uint32_t kBuf = 2 * kPlane;      // a block: low + high planes
-    static constexpr int kDma = int(kBuf / 64 / NW);  // DMA instructions per wave per block
-    static constexpr int kStores = 2 << LR;           // store instructions per wave per block
-    static_assert(K >= 3 && K <= 8 && P::kThreads == NT, "streaming pass shape");
-    static_assert(kPlane % 64 == 0 && kDma * NW * 64 == int(kBuf), "DMA instructions tile the buffer");
-};
-template <int K, int FLAGS>
-struct StreamLds {
-    static constexpr bool I = FLAGS & kIfft, F = FLAGS & kFft;
-    static constexpr uint32_t oBuf = 0, oPlane = Stream<K>::kBuf, oI = oPlane + Stream<K>::kPlane;
-    static constexpr uint32_t oF = oI + (I ? 20u << K : 0u);
-    static constexpr uint32_t words = oF + (F ? 20u << K : 0u);
-    static constexpr size_t bytes() { return size_t(words) * 4; }
-};
-
-// s_waitcnt vmcnt(N): the streaming pass counts its own DMA and store
-// instructions (the compiler does not see that LDS data waits on an LDS-DMA);
-// every one of them is issued unconditionally, and tests/test_isa.py checks
-// the built code object's counts
-template <int N>
-__device__ __forceinline__ void stream_vm_wait() {
-    static_assert(N >= 0 && N < 64, "vmcnt range");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// 8 LDS-DMA dwords into consecutive 256-byte pieces of LDS from `dst` (bytes).
-// By inline asm, one statement: it issues exactly its instructions (the vmcnt
-// counts rely on it), and hipcc sees no LDS-DMA -- with the builtin it puts a
-// vmcnt(0) before LDS reads it cannot prove apart from a pending DMA (the
-// twiddle tables), which drains the block in flight.  M0 (the DMA's LDS base)
-// is set, stepped and restored inside the statement (MI355X guide: M0 is
-// compiler-reserved; an SALU write of M0 needs one wait state before a DMA)
-__device__ __forceinline__ void dma8(uint32_t dst, const uint8_t *p0, const uint8_t *p1, const uint8_t *p2,
-                                     const uint8_t *p3, const uint8_t *p4, const uint8_t *p5, const uint8_t *p6,
-                                     const uint8_t *p7) {
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-        "global_load_lds_dword %2, off\n\ts_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
-        "global_load_lds_dword %3, off\n\ts_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
-        "global_load_lds_dword %4, off\n\ts_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
-        "global_load_lds_dword %5, off\n\ts_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
-        "global_load_lds_dword %6, off\n\ts_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
-        "global_load_lds_dword %7, off\n\ts_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
-        "global_load_lds_dword %8, off\n\ts_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
-        "global_load_lds_dword %9, off\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "s"(dst), "v"(p0), "v"(p1), "v"(p2), "v"(p3), "v"(p4), "v"(p5), "v"(p6), "v"(p7)
-        : "memory", "scc");
-}
-
-// Issue block bx's rows into `buf` (kDma LDS-DMA instructions per wave).  Lane
-// l of the wave's instruction q fills buffer word x = (wave * kDma + q) * 64 + l:
-// row lrow = (x % kPlane) / SP of the set, pack slice * SP + x % SP, its low word
-// (first plane) or high word (+32 bytes); rows and packs outside the matrices
-// read the zero line.
-template <int K>
-__device__ __forceinline__ void stream_dma(const PassArgs &A, uint32_t bx, uint32_t *buf, uint32_t lane,
-                                           uint32_t wave) {
-    using S = Stream<K>;
-#ifdef RS_PROBE_SKIP_DMA  // tools/pass5_probe.hip: a streaming pass without its row loads
-    return;
-#endif
-    const uint32_t slice = bx % A.slices, set = A.set_base + bx / A.slices;
-    const uint32_t s_lo = set & ((1u << A.a) - 1u), s_hi = set >> A.a;
-    const uint32_t pk0 = slice * S::SP;
-    // the rows' matrix: the work buffer (every row) or the source rows [rb, rb + nr)
-    const uint8_t *base = A.work_in ? A.work_in : A.src[0].base;
-    const uint64_t stride = A.work_in ? A.work_stride : A.src[0].stride;
-    const uint32_t rb = A.work_in ? 0u : A.src[0].row_begin;
-    const uint32_t nr = A.work_in ? 0xFFFFFFFFu : A.src[0].row_end - A.src[0].row_begin;
-    // the buffer's LDS byte address (the LDS-DMA destination base)
-    const uint32_t lds_base =
-        uint32_t(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint32_t *)buf));
-    const uint8_t *p[S::kDma];
-    static_for<0, S::kDma>([&](auto qc) {
-        constexpr uint32_t q = decltype(qc)::value;
-        const uint32_t x0 = (wave * uint32_t(S::kDma) + q) * 64u;  // uniform
-        const uint32_t x = x0 + lane;
-        const uint32_t hi = x0 >= S::kPlane ? 32u : 0u;
-        const uint32_t xr = x & (S::kPlane - 1u);
-        const uint32_t pk = pk0 + (xr & (S::SP - 1u));
-        const uint32_t r = s_lo + ((xr >> S::SPL) << A.a) + (s_hi << (A.a + K));
-        const uint32_t off = (pk >> 3) * 64u + (pk & 7u) * 4u + hi;
-        const bool ok = pk < A.packs && r - rb < nr;
-        p[q] = ok ? base + uint64_t(r - rb) * stride + off : A.zeros;
-    });
-    // The DMA instructions by inline asm, 8 per statement: each statement issues
-    // exactly its instructions (the vmcnt counts rely on it), and hipcc sees no
-    // LDS-DMA -- with the builtin it puts a vmcnt(0) before LDS reads it cannot
-    // prove apart from a pending DMA (the twiddle tables), which drains the
-    // block in flight.  The wave's instructions fill consecutive 256-byte pieces
-    // of the buffer: M0 (the DMA's LDS base) steps by 0x100, set and restored
-    // inside the statement (MI355X guide: M0 is compiler-reserved; an SALU
-    // write of M0 needs one wait state before the DMA reads it)
-    static_assert(S::kDma % 8 == 0, "DMA statements of 8 instructions");
-    static_for<0, S::kDma / 8>([&](auto gc) {
-        constexpr int g = decltype(gc)::value;
-        dma8(lds_base + (wave * uint32_t(S::kDma) + 8u * g) * 256u, p[8 * g], p[8 * g + 1], p[8 * g + 2],
-             p[8 * g + 3], p[8 * g + 4], p[8 * g + 5], p[8 * g + 6], p[8 * g + 7]);
-    });
-}
-
-// The 16 row-word stores of a lane in one statement (issued together, exactly
-// 16: the vmcnt counts rely on it); the data registers are read at issue
-// (single dwords).  p[i]: row i's low word; its high word is 32 bytes on.
-__device__ __forceinline__ void store16(uint8_t *const (&p)[8], const uint32_t (&lo)[8], const uint32_t (&hi)[8]) {
-    uint8_t *p0 = p[0], *p1 = p[1], *p2 = p[2], *p3 = p[3], *p4 = p[4], *p5 = p[5], *p6 = p[6], *p7 = p[7];
-    asm volatile(
-        "global_store_dword %0, %8, off\n\tglobal_store_dword %0, %16, off offset:32\n\t"
-        "global_store_dword %1, %9, off\n\tglobal_store_dword %1, %17, off offset:32\n\t"
-        "global_store_dword %2, %10, off\n\tglobal_store_dword %2, %18, off offset:32\n\t"
-        "global_store_dword %3, %11, off\n\tglobal_store_dword %3, %19, off offset:32\n\t"
-        "global_store_dword %4, %12, off\n\tglobal_store_dword %4, %20, off offset:32\n\t"
-        "global_store_dword %5, %13, off\n\tglobal_store_dword %5, %21, off offset:32\n\t"
-        "global_store_dword %6, %14, off\n\tglobal_store_dword %6, %22, off offset:32\n\t"
-        "global_store_dword %7, %15, off\n\tglobal_store_dword %7, %23, off offset:32"
-        :
-        : "v"(p0), "v"(p1), "v"(p2), "v"(p3), "v"(p4), "v"(p5), "v"(p6), "v"(p7), "v"(lo[0]), "v"(lo[1]),
-          "v"(lo[2]), "v"(lo[3]), "v"(lo[4]), "v"(lo[5]), "v"(lo[6]), "v"(lo[7]), "v"(hi[0]), "v"(hi[1]), "v"(hi[2]),
-          "v"(hi[3]), "v"(hi[4]), "v"(hi[5]), "v"(hi[6]), "v"(hi[7])
-        : "memory");
-}
-
-// Store the lane's rows (phase PH): every store is issued; rows outside the
-// destination write the junk line.
-template <int K, int PH>
-__device__ __forceinline__ void stream_store(const PassArgs &A, const Ctx &c, const uint32_t (&lo)[8],
-                                             const uint32_t (&hi)[8]) {
-    using P = typename Stream<K>::P;
-    static_assert(Stream<K>::kStores == 16, "one statement of 16 stores");
-    uint8_t *pr[8];
-    static_for<0, 8>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        const uint32_t r = c.grow(P::template lrow<PH>(c.g, i), K);
-        uint8_t *p;
-        bool ok = c.pk_ok;
-        if (A.work_out) {
-            p = A.work_out + uint64_t(r) * A.work_stride + c.pk_off;
-        } else {
-            ok = ok && r >= A.dst.row_begin && r < A.dst.row_end;
-            p = const_cast<uint8_t *>(A.dst.base) + uint64_t(r - A.dst.row_begin) * A.dst.stride + c.pk_off;
-        }
-        pr[i] = ok ? p : A.junk;
-    });
-    store16(pr, lo, hi);
-}
-
-template <int K, int FLAGS>
-__device__ __forceinline__ void stream_body(const PassArgs &A, uint32_t *lds) {
-    using S = Stream<K>;
-    using P = typename S::P;
-    using L = StreamLds<K, FLAGS>;
-    constexpr bool DO_IFFT = FLAGS & kIfft, DO_FFT = FLAGS & kFft;
-    constexpr int PL = P::NPH - 1;  // phase after an IFFT / before an FFT
-    const uint32_t nblk = A.slices * A.nsets;
-    const uint32_t b0 = uint32_t(uint64_t(blockIdx.x) * nblk / gridDim.x);
-    const uint32_t b1 = uint32_t(uint64_t(blockIdx.x + 1) * nblk / gridDim.x);
-    if (b0 >= b1) return;  // (uniform: the whole workgroup)
-    const uint32_t lane = threadIdx.x & 63u, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint32_t *buf = lds + L::oBuf, *plane = lds + L::oPlane, *tabI = lds + L::oI, *tabF = lds + L::oF;
-    // the twiddles of bx's set (normal loads: the compiler waits for them, and
-    // with an LDS-DMA in flight it waits for everything -- once per set)
-    auto stage = [&](uint32_t bx) {
-        const Ctx c = make_ctx<K, S::LR, S::SPL>(A, bx);
-        Stager<K, S::NT> st;
-        st.tabI = DO_IFFT ? tabI : nullptr;
-        st.tabF = DO_FFT ? tabF : nullptr;
-        st.load(A, c, 0);
-        st.store();
-    };
-    uint32_t staged = b0 / A.slices;
-    stage(b0);
-    stream_dma<K>(A, b0, buf, lane, wave);
-    for (uint32_t bx = b0; bx < b1; ++bx) {
-        if (bx / A.slices != staged) {  // a new set: its tables (no wave reads the old ones any more)
-            staged = bx / A.slices;
-            block_sync<true>();
-            stage(bx);
-        }
-        // this block's DMA is done once at most the last block's stores are outstanding
-        if (bx > b0) stream_vm_wait<S::kStores>();
-        else stream_vm_wait<0>();
-        block_sync<true>();  // every wave's DMA of the block (and the tables) in LDS
-        Ctx c = make_ctx<K, S::LR, S::SPL>(A, bx);
-        // the lane's row group and pack look new each block: the compiler would
-        // otherwise keep every address derived from them (LDS offsets of all
-        // phases, row addresses) in registers across the loop and spill
-        if constexpr (P::kUniform) asm volatile("" : "+v"(c.p));
-        else asm volatile("" : "+v"(c.p), "+v"(c.g));
-        uint32_t lo[8], hi[8];
-        constexpr int PH0 = DO_IFFT ? 0 : PL;
-        static_for<0, 8>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            const uint32_t x = P::template lrow<PH0>(c.g, i) * S::SP + c.p;
-            lo[i] = buf[x];
-            hi[i] = buf[S::kPlane + x];
-        });
-        block_sync<true>();  // every wave has its rows: the buffer takes the next block
-        if (bx + 1 < b1) stream_dma<K>(A, bx + 1, buf, lane, wave);
-        if constexpr (DO_IFFT) transform<K, S::LR, S::SPL, true, 2>(c, plane, tabI, lo, hi);
-        if constexpr (DO_FFT) {
-            transform<K, S::LR, S::SPL, false, 2>(c, plane, tabF, lo, hi);
-            stream_store<K, 0>(A, c, lo, hi);
-        } else {
-            stream_store<K, PL>(A, c, lo, hi);
-        }
-    }
-}
-
-template <int K, int FLAGS>
-__global__ void __launch_bounds__(512, 4) k_stream(const PassArgs A) {  // two workgroups per CU: 4 waves per SIMD
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    stream_body<K, FLAGS>(A, lds);
-}
-
-// workgroups per CU: two, as their LDS allows
-template <int K, int F>
-constexpr uint32_t stream_per_cu() { return StreamLds<K, F>::bytes() <= 80 * 1024 ? 2u : 1u; }
-
-template <int K, int F>
-hipError_t launch_stream_f(const PassArgs &A, uint32_t cus, hipStream_t s) {
-    const size_t lds = StreamLds<K, F>::bytes();
-    static std::atomic<uint64_t> attr_devs{0};  // devices whose attribute is set
-    hipError_t e = lds_attr_once(attr_devs, reinterpret_cast<const void *>(&k_stream<K, F>), int(lds));
-    if (e != hipSuccess) return e;
-    PassArgs B = A;
-    B.slices = (A.packs + Stream<K>::SP - 1) / Stream<K>::SP;
-    const uint64_t nblk = uint64_t(B.slices) * B.nsets, slots = uint64_t(cus) * stream_per_cu<K, F>();
-    const uint32_t grid = uint32_t(nblk < slots ? nblk : slots);
-    k_stream<K, F><<<grid, Stream<K>::NT, lds, s>>>(B);
-    snprintf(launch_name_buf(), kLaunchNameBytes, "k_stream<%d, %d>", K, F);
-    return hipGetLastError();
-}
-
-template <int K>
-hipError_t launch_stream_k(int flags, const PassArgs &A, uint32_t cus, hipStream_t s) {
-    switch (flags) {
-        case kIfft: return launch_stream_f<K, kIfft>(A, cus, s);
-        case kFft: return launch_stream_f<K, kFft>(A, cus, s);
-        case kIfft | kFft: return launch_stream_f<K, kIfft | kFft>(A, cus, s);
-        default: return hipErrorInvalidValue;
-    }
-}
-
 template <int K, int LR, int SPL, int F>
 hipError_t launch_f(const PassArgs &A, hipStream_t s) {
     using P = Pass<K, LR, SPL>;
@@ -1281,33 +897,6 @@ hipError_t launch_pass(int K, int flags, const PassArgs &A, hipStream_t s) {
         case 6: return launch_shape<6>(narrow, flags, A, s);
         case 7: return launch_shape<7>(narrow, flags, A, s);
         case 8: return launch_shape<8>(narrow, flags, A, s);
-        default: return hipErrorInvalidValue;
-    }
-}
-
-bool stream_supported(int K, int flags, const PassArgs &A) {
-    if (K < 3 || K > 8 || !A.zeros || !A.junk) return false;
-    if (flags != kIfft && flags != kFft && flags != (kIfft | kFft)) return false;
-    // one chunk, no decode stages, no block masks; whole 64-byte blocks, one source
-    if (A.in_chunks != 1 || A.out_chunks != 1 || A.grid_chunks != 1 || A.load_scale || A.fd_mode || A.xor_in ||
-        A.reveal || A.blk_masks)
-        return false;
-    if (A.fmt.full_packs != 0xFFFFFFFFu || A.fmt.io_bytes || (!A.work_in && A.nsrc != 1)) return false;
-    // enough blocks that every CU walks a run of them (PassArgs::stream_min_blocks)
-    const uint32_t sp = 1u << (12 - K);
-    const uint64_t blocks = uint64_t((A.packs + sp - 1) / sp) * A.nsets;
-    return blocks >= A.stream_min_blocks;
-}
-
-hipError_t launch_stream(int K, int flags, const PassArgs &A, uint32_t cus, hipStream_t s) {
-    if (!stream_supported(K, flags, A) || cus == 0) return hipErrorInvalidValue;
-    switch (K) {
-        case 3: return launch_stream_k<3>(flags, A, cus, s);
-        case 4: return launch_stream_k<4>(flags, A, cus, s);
-        case 5: return launch_stream_k<5>(flags, A, cus, s);
-        case 6: return launch_stream_k<6>(flags, A, cus, s);
-        case 7: return launch_stream_k<7>(flags, A, cus, s);
-        case 8: return launch_stream_k<8>(flags, A, cus, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -138,7 +138,6 @@ _sig("rs_check_device", _int, _vp)
 
 
 _sig("rs_mono_enable", _int, _vp, _int)
-_sig("rs_stream_enable", _int, _vp, _int)
 _sig("rs_release_stream_scratch", _int, _vp, _vp)
 
 
@@ -156,14 +155,6 @@ def mono_enable(enable=True, ctx=None) -> None:
     packs only, + 16 2-element packs everywhere (rs_mono_enable)."""
     ctx = ctx or default_context()
     _lib.rs_mono_enable(ctx.handle, int(enable))
-
-
-def stream_enable(mode=1, ctx=None) -> None:
-    """Streaming pass kernel for large matrices: 0 = never, 1 = passes of >= 4096 blocks
-    (default), 2 = wherever the pass's shape is supported (rs_stream_enable)."""
-    ctx = ctx or default_context()
-    if _lib.rs_stream_enable(ctx.handle, int(mode)) != 0:
-        raise ValueError("stream mode must be 0, 1 or 2")
 
 
 def check_device(ctx=None) -> None:

@@ -1,19 +1,12 @@
 """Checks of the built gfx950 code object (CPU: disassembly, no GPU).
 
-Two kernels wait for memory by counts the compiler does not derive itself:
-
-* k_stream (rs_kernels.hip): its rows arrive by LDS-DMA (inline asm, so hipcc
-  does not see them) and it waits for a block's DMA with s_waitcnt vmcnt(N),
-  N = the store instructions issued after that DMA.  That is exact only if
-  every DMA and store instruction is issued whenever its site runs: the DMAs
-  come in asm statements of 8 global_load_lds_dword, the stores in one of 16
-  global_store_dword, and no branch may jump over part of one.
-* the staged decode column kernel (rs_mono.hip) loads lw_fold first and has
-  the compiler place the wait for it at its first use, after eval_poly's first
-  transform; on the path that issues the row and table loads that wait must
-  leave them in flight (vmcnt(13) in the headline decode: 1 shared-table load,
-  4 row loads, 8 phase-1 table loads issued after lw_fold).  A smaller count
-  would still be correct but would hold eval_poly until the rows land.
+rs_mono.hip's staged decode loads lw_fold first, with a plain load the compiler
+tracks, and lets the compiler place the wait for it at its first use, after
+eval_poly's first transform.  On the path that issues the row and table loads
+that wait must leave them in flight: vmcnt(13) in the headline decode (1
+shared-table load, 4 row loads, 8 phase-1 table loads issued after lw_fold).
+A smaller count would still be correct but would hold eval_poly until the rows
+land (the former hand-counted inline-asm wait).
 """
 import os
 import re
@@ -67,38 +60,6 @@ def _disassemble(tmp_path_factory):
 @pytest.fixture(scope="module")
 def kernels(tmp_path_factory):
     return _disassemble(tmp_path_factory)
-
-
-def _partly_skipped(body, site):
-    """Whether some forward branch jumps over part (not all) of a site's instructions."""
-    addrs = [body[j][0] for j in site]
-    for a, ins, t in body:
-        if t is not None and a is not None and (ins.startswith("s_cbranch") or ins.startswith("s_branch")):
-            n = sum(a < x < t for x in addrs)
-            if 0 < n < len(addrs):
-                return True
-    return False
-
-
-def test_stream_kernels_issue_every_counted_instruction(kernels):
-    stream = {k: v for k, v in kernels.items() if "8k_stream" in k}
-    assert len(stream) >= 15, sorted(stream)
-    for name, body in stream.items():
-        dma = [i for i, (_, ins, _) in enumerate(body) if ins.startswith("global_load_lds_dword")]
-        stores = [i for i, (_, ins, _) in enumerate(body) if ins.startswith("global_store_dword")]
-        # two DMA sites (before the loop, in it) of two 8-instruction statements, one 16-store statement
-        assert len(dma) == 32 and len(stores) == 16, (name, len(dma), len(stores))
-        groups = [dma[g:g + 8] for g in range(0, 32, 8)]
-        for grp in groups:  # one asm statement: nothing but M0 steps between its DMAs
-            between = [body[j][1] for j in range(grp[0], grp[-1] + 1) if j not in grp]
-            assert all(b.startswith("s_add_u32 m0") or b.startswith("s_nop") for b in between), (name, between)
-        assert stores == list(range(stores[0], stores[0] + 16)), name
-        # no branch skips part of a group: each instruction is issued whenever its statement runs
-        for grp in groups + [stores]:
-            assert not _partly_skipped(body, grp), (name, grp[0])
-        # the block waits: vmcnt(16) (the last block's stores outstanding) and vmcnt(0)
-        waits = {int(m.group(1)) for _, ins, _ in body for m in [re.match(r"s_waitcnt vmcnt\((\d+)\)$", ins)] if m}
-        assert 16 in waits and 0 in waits, (name, waits)
 
 
 def test_headline_decode_leaves_row_loads_in_flight(kernels):

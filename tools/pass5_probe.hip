@@ -2,7 +2,7 @@
 // 32768:32768 x 64 KiB HighRate encode (IFFT level 0, K = 8 from the originals;
 // fused IFFT + FFT top level, K = 7; FFT level 0, K = 8 to the recovery rows),
 // each timed back to back with HIP events, plus a 2 GiB device copy.
-// Build variants with -D flags of rs_kernels.hip (tools/ab_dec.sh-style A/B).
+// Build variants with -D flags of rs_kernels.hip (A/B; profiles/r04a/ab_stream_pass.md).
 // Run: tools/_probe/pass5_<variant> [rows] [shard bytes] [iters]
 #include "../reed-solomon-simd_amd/csrc/rs_kernels.hip"
 
@@ -91,52 +91,26 @@ int main(int argc, char **argv) {
     const size_t n16 = bytes / 16;
     const double tc = time_us([&] { k_copy<<<8192, 256>>>((const uint4 *)orig, (uint4 *)rec, n16); }, iters);
     printf("copy 2x%zu B  %9.1f us  %6.2f TB/s\n", bytes, tc, gb / tc * 1e3);
-    // the streaming pass (k_stream) beside the one-block-per-workgroup pass (k_pass)
-    uint8_t *zeros;
-    CK(hipMalloc(&zeros, 512));
-    CK(hipMemset(zeros, 0, 512));
-    int cus = 0;
-    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-    for (rs::PassArgs *X : {&P, &Q, &F}) X->zeros = zeros, X->junk = zeros + 256, X->cus = uint32_t(cus);
-    for (int stream = 0; stream < 2; ++stream) {
-        auto run = [&](const char *name, int K, int flags, const rs::PassArgs &X) {
-            const bool st = stream && rs::stream_supported(K, flags, X);
-            const double t = time_us([&] { CK(st ? rs::launch_stream(K, flags, X, X.cus, 0) : rs::launch_pass(K, flags, X, 0)); }, iters);
-            printf("%-10s K=%d  %9.1f us  %6.2f TB/s  (%s)\n", name, K, t, gb / t * 1e3, rs::launch_name_buf());
-            return t;
-        };
-        const double t1 = run("ifft", K0, rs::kIfft, P);
-        const double t2 = run("ifft+fft", K1, rs::kIfft | rs::kFft, Q);
-        const double t3 = run("fft", K0, rs::kFft, F);
-        printf("encode (3 passes%s) %9.1f us  %7.1f GiB/s\n", stream ? ", streaming" : "", t1 + t2 + t3,
-               2.0 * bytes / (t1 + t2 + t3) * 1e6 / (1u << 30));
-    }
-    // parity of the streaming passes against k_pass on this shape (whole recovery matrix)
-    {
-        uint8_t *rec2;
-        CK(hipMalloc(&rec2, bytes));
+    auto run = [&](const char *name, int K, int flags, const rs::PassArgs &X) {
+        const double t = time_us([&] { CK(rs::launch_pass(K, flags, X, 0)); }, iters);
+        printf("%-10s K=%d  %9.1f us  %6.2f TB/s  (%s)\n", name, K, t, gb / t * 1e3, rs::launch_name_buf());
+        return t;
+    };
+    const double t1 = run("ifft", K0, rs::kIfft, P);
+    const double t2 = run("ifft+fft", K1, rs::kIfft | rs::kFft, Q);
+    const double t3 = run("fft", K0, rs::kFft, F);
+    printf("encode (3 passes) %9.1f us  %7.1f GiB/s\n", t1 + t2 + t3, 2.0 * bytes / (t1 + t2 + t3) * 1e6 / (1u << 30));
+    {  // FNV-1a of the recovery rows: compare across -D variants of rs_kernels.hip
         CK(hipMemset(W, 0, bytes));
         CK(rs::launch_pass(K0, rs::kIfft, P, 0));
         CK(rs::launch_pass(K1, rs::kIfft | rs::kFft, Q, 0));
         CK(rs::launch_pass(K0, rs::kFft, F, 0));
-        CK(hipMemcpy(rec2, rec, bytes, hipMemcpyDeviceToDevice));
-        CK(hipMemset(W, 0, bytes));
-        CK(hipMemset(rec, 0, bytes));
-        auto go = [&](int K, int fl, const rs::PassArgs &X) {
-            CK(rs::stream_supported(K, fl, X) ? rs::launch_stream(K, fl, X, X.cus, 0) : rs::launch_pass(K, fl, X, 0));
-        };
-        go(K0, rs::kIfft, P);
-        go(K1, rs::kIfft | rs::kFft, Q);
-        go(K0, rs::kFft, F);
         CK(hipDeviceSynchronize());
-        std::vector<uint8_t> a(bytes), b(bytes);
-        CK(hipMemcpy(a.data(), rec, bytes, hipMemcpyDeviceToHost));
-        CK(hipMemcpy(b.data(), rec2, bytes, hipMemcpyDeviceToHost));
-        uint64_t h = 0xcbf29ce484222325ull;  // FNV-1a of the k_pass recovery rows (compare across -D variants)
+        std::vector<uint8_t> b(bytes);
+        CK(hipMemcpy(b.data(), rec, bytes, hipMemcpyDeviceToHost));
+        uint64_t h = 0xcbf29ce484222325ull;
         for (uint8_t v : b) h = (h ^ v) * 0x100000001b3ull;
-        printf("k_pass recovery hash %016llx\n", (unsigned long long)h);
-        printf("streaming vs k_pass recovery rows: %s\n", a == b ? "identical" : "DIFFER");
-        if (a != b) return 1;
+        printf("recovery hash %016llx\n", (unsigned long long)h);
     }
     return 0;
 }
