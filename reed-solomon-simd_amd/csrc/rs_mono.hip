@@ -1525,10 +1525,10 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             // Decodes: eval_poly's inputs first.  Thread t's erased / received bits
             // (rows 2t, 2t + 1) are in word t / 16 of the bitmaps: the wave's 4 words
             // are uniform, i.e. scalar loads of the kernel arguments.  Its lw_fold
-            // pair is the first vector load, issued by inline asm, so the compiler's
-            // vmcnt waits do not know it: col_eval_poly waits for it by an explicit
-            // count of the vector loads issued after it (rows and table pieces, all
-            // unconditional), leaving those in flight while eval_poly runs
+            // pair is the first vector load, a plain load the compiler tracks: its
+            // wait sits at the first use in col_eval_poly, after the rows and table
+            // pieces are issued, and leaves those in flight while eval_poly runs
+            // (vmcnt(13) in the headline decode, checked by tests/test_isa.py)
             uint32_t ebits = 0, rbits = 0, lwv = 0;
             if constexpr (DEC) {  // the staged decode always evaluates eval_poly itself
                 const uint32_t g = lane >> 4, sh = (2u * lane) & 31u;
