@@ -386,6 +386,20 @@ def stripe_bench(args, rs, ctx, config, world, rank, dev):
         host_e2e = {"encode_GiBps": round(world * step_bytes / best[1] / 2**30, 3),
                     "decode_1pct_GiBps": round(world * step_bytes / ddt / 2**30, 3), "slices": best[0],
                     "note": "pinned host buffers, hipMemcpy2DAsync in + kernels + out, column slices over 3 streams"}
+        # the host link's own floor for this call: one synchronous pinned copy of the
+        # originals in and one of the recovery rows out, at these sizes (latency included)
+        # plus the kernel, against the measured encode; and the link's bulk rate
+        h2d_in, _ = host_link(dev, N * S)
+        _, d2h_out = host_link(dev, M * S)
+        bulk_h2d, bulk_d2h = host_link(dev, 256 << 20, reps=5)
+        floor = h2d_in + d2h_out + gpu_t / args.steps
+        host_e2e["link"] = {"h2d_us": round(h2d_in * 1e6, 2), "d2h_us": round(d2h_out * 1e6, 2),
+                            "floor_us": round(floor * 1e6, 2), "encode_us": round(best[1] * 1e6, 2),
+                            "frac_of_floor": round(floor / best[1], 3),
+                            "bulk_h2d_GBps": round((256 << 20) / bulk_h2d / 1e9, 2),
+                            "bulk_d2h_GBps": round((256 << 20) / bulk_d2h / 1e9, 2),
+                            "note": "floor = one pinned copy in (N*S) + one out (M*S), each synchronous, "
+                                    "+ the device encode; bulk = 256 MiB copies"}
 
     # ---- the drop-in object API (rank 0): ReedSolomonEncoder / Decoder calls as
     # the reference's benchmark makes them, through the C ABI in native code ----
@@ -440,6 +454,26 @@ def object_api_bench(N, M, S, iters, warmup):
     r["note"] = ("C ABI from native code: add shards (host, pinned staging) + encode/decode; one stream, "
                  "received rows in, recovery/restored rows out (PCIe included)")
     return r
+
+
+def host_link(dev, nbytes, reps=50):
+    """Seconds per synchronous pinned host->device and device->host copy of nbytes."""
+    import torch
+
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    out = []
+    for fwd in (True, False):
+        for i in range(reps + 2):
+            if i == 2:
+                t0 = time.perf_counter()
+            if fwd:
+                d.copy_(h, non_blocking=True)
+            else:
+                h.copy_(d, non_blocking=True)
+            torch.cuda.synchronize()
+        out.append((time.perf_counter() - t0) / reps)
+    return out[0], out[1]
 
 
 def device_copy(dev):

@@ -637,14 +637,13 @@ __device__ __forceinline__ Ctx make_ctx(const PassArgs &A, uint32_t bx) {
 // erasure vector -> Walsh-Hadamard -> x lw_fold -> Walsh-Hadamard, all mod
 // 65535, the butterfly partners across lanes; row info into LDS.
 template <int K>
-__device__ __forceinline__ void pass_eval_poly(const PassArgs &A, uint32_t *rinfo) {
+__device__ __forceinline__ void pass_eval_poly(const PassArgs &A, uint32_t *rinfo, uint32_t lw) {
     static_assert((1 << K) <= int(kPassEvalRows), "one wave holds the points");
     const uint32_t i = threadIdx.x;
     if (i < 64) {
         constexpr uint32_t n = 1u << K;
         auto am = [](uint32_t a, uint32_t b) { const uint32_t s = a + b; return (s + (s >> 16)) & 0xFFFFu; };
         auto sm = [](uint32_t a, uint32_t b) { const uint32_t d = a - b; return (d + (d >> 16)) & 0xFFFFu; };
-        const uint32_t lw = i < n ? uint32_t(A.ev_lw_fold[i]) : 0u;
         const uint32_t e = i < n ? (A.ev_erased[i >> 5] >> (i & 31u)) & 1u : 0u;
         // high rate: v = e;  low rate: v = e - 1 on [0, end), 0 beyond  (mod 65535)
         uint32_t v = A.ev_low_rate ? (i < A.ev_end ? (e ? 0u : 65534u) : 0u) : e;
@@ -707,13 +706,21 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
     uint32_t lo[P::R], hi[P::R];
     uint32_t xl[XOR_IN ? P::R : 1], xh[XOR_IN ? P::R : 1];
     // loads first, then table staging: one barrier covers both latencies
+    // fused eval_poly: its lw_fold values are the first load
+    const uint32_t lwv = EVAL && threadIdx.x < (1u << K) ? uint32_t(A.ev_lw_fold[threadIdx.x]) : 0u;
     load_rows<K, LR, SPL, DO_IFFT ? 0 : PL, SCALE, EVAL>(A, c, A.in_chunk0 ? 0u : gchunk, lo, hi);
     if constexpr (XOR_IN) load_xor_rows<K, LR, SPL, PL>(A, c, xl, xh);
     {
         auto st = stager_for<K, LR, SPL, FLAGS>(lds);
         if constexpr (EVAL) {
-            pass_eval_poly<K>(A, rinfo);
+            // twiddles in flight while eval_poly runs; then the row tables it indexes
+            auto tw = st;
+            tw.tabS = tw.tabV = nullptr;
+            tw.load(A, c, gchunk);
+            pass_eval_poly<K>(A, rinfo, lwv);
+            tw.store();
             __syncthreads();
+            st.tabI = st.tabF = nullptr;
             st.ri_lds = rinfo;
         }
         st.load(A, c, gchunk);

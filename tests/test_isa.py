@@ -80,3 +80,20 @@ def test_headline_decode_leaves_row_loads_in_flight(kernels):
                     break
     # skip path (the shared-table load only after it: 1), live path (13 loads after it)
     assert 13 in waits, waits
+
+
+def test_every_staged_decode_waits_for_lw_fold(kernels):
+    """Every staged decode instantiation (L = 7..11, plain and split plans, 2- and 4-element
+    packs): each multiply that reads the lw_fold register (the first vector load's
+    destination) comes after an s_waitcnt vmcnt, placed by the compiler."""
+    dec = [k for k in kernels if re.search(r"k_monoILi\d+ELi1ELi2ELb1E", k)]
+    assert len(dec) >= 10, sorted(dec)
+    for name in dec:
+        body = [ins for _, ins, _ in kernels[name]]
+        first = next(i for i, ins in enumerate(body) if ins.startswith("global_load_dword "))
+        reg = body[first].split()[1].rstrip(",")
+        uses = [i for i in range(first + 1, len(body))
+                if body[i].startswith("v_mul") and re.search(r"\b%s\b" % re.escape(reg), body[i])]
+        assert uses, name
+        for i in uses:
+            assert any(re.match(r"s_waitcnt vmcnt\(\d+\)", body[j]) for j in range(first + 1, i)), (name, i)
