@@ -111,25 +111,6 @@ __global__ void __launch_bounds__(1024) k_eval_poly(const EvalArgs A) {
 // reduction mod 65535 (values below B_k after k layers, folded at the end).
 // It replaces 22 one-layer barriers (2^11: 8.2 -> 3.2..5.0 us per launch) or
 // three launches (2^12: 10.0 -> 5.0 us; tools/eval_probe.hip, profiles/r03b).
-template <int J>
-__device__ __forceinline__ uint32_t ev_lane_xor(uint32_t v, uint32_t lane) {  // value of lane ^ 2^J
-    if constexpr (J == 4) {
-        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-        return (lane & 16u) ? r[0] : r[1];
-    } else if constexpr (J == 5) {
-        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-        return (lane & 32u) ? r[0] : r[1];
-    } else if constexpr (J == 0) {
-        return __builtin_amdgcn_update_dpp(0, int(v), 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
-    } else if constexpr (J == 1) {
-        return __builtin_amdgcn_update_dpp(0, int(v), 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
-    } else if constexpr (J == 2) {  // row_half_mirror of quad_perm 3,2,1,0
-        return __builtin_amdgcn_update_dpp(0, __builtin_amdgcn_update_dpp(0, int(v), 0x1B, 0xF, 0xF, false), 0x141,
-                                           0xF, 0xF, false);
-    } else {
-        return __builtin_amdgcn_update_dpp(0, int(v), 0x128, 0xF, 0xF, false);  // row_ror:8
-    }
-}
 constexpr uint64_t ev_bound(int k) {  // B_k: values stay below it after k lazy layers
     uint64_t b = 65536u;
     for (int i = 0; i < k; ++i) b = 2 * b + 65535u;
@@ -165,7 +146,7 @@ __device__ __forceinline__ void walsh_fast(uint32_t (&x)[1 << LV], uint32_t *buf
         const uint32_t m = (lane & (1u << J)) ? ~0u : 0u, c = m & kEvM1<LV + J>;
         static_for<0, V>([&](auto vc) {
             constexpr int v = decltype(vc)::value;
-            x[v] = ev_lane_xor<J>(x[v], lane) + (x[v] ^ m) + c;
+            x[v] = lane_xor<J>(x[v], lane) + (x[v] ^ m) + c;
         });
     });
     static_for<0, 2>([&](auto rc) {  // wave bits: thread bits 6 + 2 rnd, 7 + 2 rnd

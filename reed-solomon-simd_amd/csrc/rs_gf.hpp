@@ -22,6 +22,32 @@ __device__ __forceinline__ void static_for(F &&f) {
     }
 }
 
+// The value of lane ^ 2^J of a wave64: DPP within rows of 16 lanes (J < 4),
+// v_permlane16/32_swap across them (no LDS traffic).
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+    if constexpr (J == 0) return __builtin_amdgcn_update_dpp(0, int(v), 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+    else if constexpr (J == 1) return __builtin_amdgcn_update_dpp(0, int(v), 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+    else if constexpr (J == 2)  // lane ^ 4 = row_half_mirror (lane ^ 7) of quad_perm 3,2,1,0 (lane ^ 3):
+        // two DPP moves instead of a ds_swizzle, whose lgkmcnt wait would also
+        // drain LDS reads in flight
+        return __builtin_amdgcn_update_dpp(0, __builtin_amdgcn_update_dpp(0, int(v), 0x1B, 0xF, 0xF, false), 0x141, 0xF,
+                                           0xF, false);
+    else return __builtin_amdgcn_update_dpp(0, int(v), 0x128, 0xF, 0xF, false);  // row_ror:8 = lane ^ 8
+}
+template <int J>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v, uint32_t lane) {
+    if constexpr (J == 4) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16u) ? r[0] : r[1];
+    } else if constexpr (J == 5) {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32u) ? r[0] : r[1];
+    } else {
+        return xor_lane<J>(v);
+    }
+}
+
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }

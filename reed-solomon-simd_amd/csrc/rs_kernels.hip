@@ -635,7 +635,8 @@ __device__ __forceinline__ Ctx make_ctx(const PassArgs &A, uint32_t bx) {
 // eval_poly of a single-pass decode (2^K <= 64 work rows, PassArgs::fused_eval)
 // in wave 0, as k_eval_poly (rs_eval.hip; reference src/engine/utils.rs:20-31):
 // erasure vector -> Walsh-Hadamard -> x lw_fold -> Walsh-Hadamard, all mod
-// 65535, the butterfly partners across lanes; row info into LDS.
+// 65535, the butterfly partners across lanes (DPP / permlane swaps); row info
+// into LDS.
 template <int K>
 __device__ __forceinline__ void pass_eval_poly(const PassArgs &A, uint32_t *rinfo, uint32_t lw) {
     static_assert((1 << K) <= int(kPassEvalRows), "one wave holds the points");
@@ -650,7 +651,7 @@ __device__ __forceinline__ void pass_eval_poly(const PassArgs &A, uint32_t *rinf
         auto walsh = [&]() {
             static_for<0, K>([&](auto hc) {
                 constexpr int h = decltype(hc)::value;
-                const uint32_t o = uint32_t(__shfl_xor(int(v), 1 << h));
+                const uint32_t o = lane_xor<h>(v, i);
                 v = (i >> h) & 1u ? sm(o, v) : am(v, o);
             });
         };
