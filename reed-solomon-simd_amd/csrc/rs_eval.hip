@@ -103,14 +103,15 @@ __global__ void __launch_bounds__(1024) k_eval_poly(const EvalArgs A) {
     RS_ESTAMP(5);
 }
 
-// 2^11 and 2^12 points (pass-kernel decodes of 2048 / 4096 work rows): one
+// 2^11 .. 2^13 points (pass-kernel decodes of 2048 .. 8192 work rows): one
 // workgroup of 1024 threads, thread t holding rows t*V .. t*V + V - 1
 // (V = 2^(u - 10)), the transform as in the column kernel's fused eval_poly
 // (rs_mono.hip col_walsh): log2(V) layers in registers, 6 across lanes by DPP /
 // v_permlane*_swap, the 4 wave bits as two LDS rounds of two layers, lazy
 // reduction mod 65535 (values below B_k after k layers, folded at the end).
 // It replaces 22 one-layer barriers (2^11: 8.2 -> 3.2..5.0 us per launch) or
-// three launches (2^12: 10.0 -> 5.0 us; tools/eval_probe.hip, profiles/r03b).
+// three launches (2^12: 10.0 -> 5.0 us, 2^13: 10.6 -> 8.3 us; tools/eval_probe.hip,
+// profiles/r03b, profiles/r04a).
 constexpr uint64_t ev_bound(int k) {  // B_k: values stay below it after k lazy layers
     uint64_t b = 65536u;
     for (int i = 0; i < k; ++i) b = 2 * b + 65535u;
@@ -124,12 +125,21 @@ __device__ __forceinline__ uint32_t ev_fold(uint32_t x) {
     return (x & 0xFFFFu) + (x >> 16);
 }
 
+// The LDS rounds keep value v of thread t at word v * 1024 + t: a wave's
+// stores and reads are 64 consecutive words.  (Thread-major, t * V + v, is a
+// V-way bank conflict: 2^13 points 10.65 -> 8.27 us, 2^12 5.02 -> 4.87 us per
+// launch, profiles/r04a/eval_vmajor_ab.txt; RS_EVAL_VMAJOR=0 for the A/B.)
+#ifndef RS_EVAL_VMAJOR
+#define RS_EVAL_VMAJOR 1
+#endif
 // One 2^(LV + 10)-point transform; G0: index of its first LDS round (rounds
 // alternate the two buffers across both transforms, so no barrier between them)
 template <int LV, int G0>
 __device__ __forceinline__ void walsh_fast(uint32_t (&x)[1 << LV], uint32_t *buf) {
     constexpr int V = 1 << LV, L = LV + 10;
     const uint32_t t = threadIdx.x, lane = t & 63u;
+    // LDS word of value v of thread q
+    auto ix = [](uint32_t q, int v) { return RS_EVAL_VMAJOR ? uint32_t(v) * 1024u + q : q * V + uint32_t(v); };
     static_for<0, LV>([&](auto kc) {  // register bits
         constexpr int k = decltype(kc)::value;
         static_for<0, V>([&](auto vc) {
@@ -156,7 +166,7 @@ __device__ __forceinline__ void walsh_fast(uint32_t (&x)[1 << LV], uint32_t *buf
         uint32_t *b = buf + ((((G0 + rnd) & 1) ^ 1) << L);
         static_for<0, V>([&](auto vc) {
             constexpr int v = decltype(vc)::value;
-            b[t * V + v] = x[v];
+            b[ix(t, v)] = x[v];
         });
         __syncthreads();
         const uint32_t m1 = (t & h1) ? ~0u : 0u, c1 = m1 & kEvM1<j>;
@@ -164,8 +174,8 @@ __device__ __forceinline__ void walsh_fast(uint32_t (&x)[1 << LV], uint32_t *buf
         const uint32_t g0 = t & ~(h1 | h2);
         static_for<0, V>([&](auto vc) {
             constexpr int v = decltype(vc)::value;
-            const uint32_t v00 = b[g0 * V + v], v01 = b[(g0 | h1) * V + v];
-            const uint32_t v10 = b[(g0 | h2) * V + v], v11 = b[(g0 | h1 | h2) * V + v];
+            const uint32_t v00 = b[ix(g0, v)], v01 = b[ix(g0 | h1, v)];
+            const uint32_t v10 = b[ix(g0 | h2, v)], v11 = b[ix(g0 | h1 | h2, v)];
             const uint32_t lo = v00 + (v01 ^ m1) + c1, hi = v10 + (v11 ^ m1) + c1;
             x[v] = lo + (hi ^ m2) + c2;
         });
@@ -204,6 +214,9 @@ __global__ void __launch_bounds__(1024) k_eval_fast(const EvalArgs A) {
 }
 #ifndef RS_EVAL_FAST_MIN_U  // (A/B: 14 = off)
 #define RS_EVAL_FAST_MIN_U 11
+#endif
+#ifndef RS_EVAL_FAST_MAX_U  // (A/B: 12 = 2^13 points on the three-launch form)
+#define RS_EVAL_FAST_MAX_U 13
 #endif
 
 // Large transforms (2^u > kEvalSingleRows) spread over many workgroups: the
@@ -274,8 +287,8 @@ __global__ void __launch_bounds__(512) k_walsh_part(const EvalArgs A, uint32_t a
 
 hipError_t launch_eval_poly(const EvalArgs &A, hipStream_t s) {
     const uint32_t n = 1u << A.u;
-    // (2^13 points measured no faster than the three launches: 10.8 vs 10.6 us)
-    if (A.u >= RS_EVAL_FAST_MIN_U && A.u <= 12) {
+    // (2^13 points: 8.3 us in one workgroup against 10.6 us in three launches)
+    if (A.u >= RS_EVAL_FAST_MIN_U && A.u <= RS_EVAL_FAST_MAX_U) {
         static_assert((1u << 13) <= kEvalInlineRows, "k_eval_fast reads the inline bitmaps");
         const size_t lds = size_t(8) * n;  // two exchange buffers of 2^u words
         static std::atomic<uint64_t> fast_devs[3] = {{0}, {0}, {0}};  // per kernel: devices set
