@@ -136,6 +136,34 @@ def test_decode_device_matches_oracle(torch, rs, rate, N, M, S, loss):
     assert np.all(got[~miss] == 0x33), "present rows of the output must not be written"
 
 
+# eval_poly forms by work rows 2^u (rs_eval.hip): one workgroup (k_eval_fast, value-major LDS
+# rounds) at u = 11..13 on the pass-kernel route, three launches (k_walsh_part) at u >= 14;
+# both rates, LowRate with end < 2^u.  (rate, N, M): u
+# (2^11 rows take the pass kernels only past the column kernel's 256 packs: 4 KiB shards)
+EVAL_DEC = [("high", 1500, 20, 11, 4096), ("low", 20, 3000, 12, 64), ("high", 2048, 2048, 12, 64),
+            ("low", 2000, 6000, 13, 64), ("high", 4096, 4096, 13, 64), ("high", 6000, 1500, 13, 64),
+            ("high", 5000, 3000, 14, 64), ("low", 3000, 9000, 14, 64)]
+
+
+@pytest.mark.parametrize("rate,N,M,u,S", EVAL_DEC)
+def test_eval_poly_forms_match_oracle(torch, rs, rate, N, M, u, S):
+    chunk = 1 << ((M if rate == "high" else N) - 1).bit_length()
+    end = chunk + (N if rate == "high" else M)
+    assert (1 << (end - 1).bit_length()) == 1 << u
+    rng = np.random.default_rng(u * 1000 + N)
+    orig = O.generate_original(N, S, u)
+    rec = O.encode(rate, orig, M)
+    L = max(1, min(N, M) // 3)
+    op = np.ones(N, np.uint8)
+    op[rng.choice(N, L, replace=False)] = 0
+    rp = np.zeros(M, np.uint8)
+    rp[rng.choice(M, L, replace=False)] = 1
+    want = O.decode(rate, orig, op, rec, rp)
+    got = gpu_decode(torch, rs, rate, orig, op, rec, rp)
+    miss = op == 0
+    assert np.array_equal(got[miss], orig[miss]) and np.array_equal(got[miss], want[miss])
+
+
 # decodes of at most 64 work rows: one pass that evaluates eval_poly itself
 # (rs_kernels.hip pass_eval_poly); (rate, N, M): work rows 2..64, both rates,
 # the LowRate end < n and the HighRate recovery padding
