@@ -283,6 +283,85 @@ __global__ void __launch_bounds__(512) k_walsh_part(const EvalArgs A, uint32_t a
     }
 }
 
+// The same steps with one wave per set of 2^K values (K = 7, 8): lane l holds
+// values j = l * V .. l * V + V - 1 (V = 2^(K - 6)); the log2(V) low layers in
+// registers, the 6 above across lanes by DPP / permlane swaps -- no LDS and no
+// barrier (k_walsh_part: one layer per barrier).  Layers run in the same order,
+// each exact mod 65535 (add_mod / sub_mod), so the values are identical.
+template <int STEP, int K>
+__global__ void __launch_bounds__(64) k_walsh_wave(const EvalArgs A, uint32_t a) {
+    constexpr int LV = K - 6, V = 1 << LV;
+    const uint32_t set = blockIdx.x, lane = threadIdx.x;
+    const uint32_t lo = set & ((1u << a) - 1u), hi = set >> a;
+    auto row = [&](int v) { return lo + ((lane * V + uint32_t(v)) << a) + (hi << (a + K)); };
+    uint32_t x[V];
+    static_for<0, V>([&](auto vc) {
+        constexpr int v = decltype(vc)::value;
+        const uint32_t i = row(v);
+        if constexpr (STEP == 0) {
+            const uint32_t e = state_bit(A, i, 0);
+            x[v] = A.low_rate ? (i < A.end ? (e ? 0u : 65534u) : 0u) : e;
+        } else {
+            x[v] = A.rowinfo[i];
+        }
+    });
+    auto walsh = [&]() {
+        static_for<0, LV>([&](auto hc) {  // register bits
+            constexpr int h = decltype(hc)::value;
+            static_for<0, V>([&](auto vc) {
+                constexpr int v = decltype(vc)::value;
+                if constexpr (!(v & (1 << h))) {
+                    const uint32_t p = x[v], q = x[v | (1 << h)];
+                    x[v] = add_mod(p, q);
+                    x[v | (1 << h)] = sub_mod(p, q);
+                }
+            });
+        });
+        static_for<0, 6>([&](auto jc) {  // lane bits
+            constexpr int J = decltype(jc)::value;
+            static_for<0, V>([&](auto vc) {
+                constexpr int v = decltype(vc)::value;
+                const uint32_t o = lane_xor<J>(x[v], lane);
+                x[v] = (lane >> J) & 1u ? sub_mod(o, x[v]) : add_mod(x[v], o);
+            });
+        });
+    };
+    walsh();
+    if constexpr (STEP == 1) {  // x lw_fold between the two transforms' high-bit layers
+        static_for<0, V>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            const uint32_t i = row(v);
+            const uint32_t p = x[v] * A.lw_fold[i];
+            uint32_t f = add_mod(p & 0xFFFFu, p >> 16);
+            if (A.low_rate && i == 0) f = add_mod(f, A.lw0);
+            x[v] = f;
+        });
+        walsh();
+    }
+    static_for<0, V>([&](auto vc) {
+        constexpr int v = decltype(vc)::value;
+        const uint32_t i = row(v);
+        uint32_t y = x[v];
+        if constexpr (STEP == 3) y |= state_bit(A, i, 1) ? 0u : 0x10000u;
+        A.rowinfo[i] = y;
+    });
+}
+
+#ifndef RS_EVAL_WAVE  // (A/B: 0 = k_walsh_part, one layer per barrier)
+#define RS_EVAL_WAVE 1
+#endif
+template <int STEP>
+void walsh_step(const EvalArgs &A, uint32_t a, uint32_t K, uint32_t n, hipStream_t s) {
+    if (RS_EVAL_WAVE && K == 7) {
+        k_walsh_wave<STEP, 7><<<n >> 7, 64, 0, s>>>(A, a);
+    } else if (RS_EVAL_WAVE && K == 8) {
+        k_walsh_wave<STEP, 8><<<n >> 8, 64, 0, s>>>(A, a);
+    } else {
+        const uint32_t m = 1u << K;
+        k_walsh_part<STEP><<<n >> K, m / 2 < 64 ? 64 : (m / 2 > 512 ? 512 : m / 2), size_t(4) * m, s>>>(A, a, K);
+    }
+}
+
 }  // namespace
 
 hipError_t launch_eval_poly(const EvalArgs &A, hipStream_t s) {
@@ -306,16 +385,12 @@ hipError_t launch_eval_poly(const EvalArgs &A, hipStream_t s) {
     }
     if (n > kEvalSingleRows) {
         const uint32_t K1 = A.u / 2, K2 = A.u - K1;
-        const auto go = [&](auto kern, uint32_t a, uint32_t K) {
-            const uint32_t m = 1u << K;
-            kern<<<n >> K, m / 2 < 64 ? 64 : (m / 2 > 512 ? 512 : m / 2), size_t(4) * m, s>>>(A, a, K);
-        };
         // Walsh-Hadamard layers on different bits commute: low bits of the
         // first transform; high bits of both around the multiply (one launch);
         // low bits of the second transform + output
-        go(k_walsh_part<0>, 0, K1);
-        go(k_walsh_part<1>, K1, K2);
-        go(k_walsh_part<3>, 0, K1);
+        walsh_step<0>(A, 0, K1, n, s);
+        walsh_step<1>(A, K1, K2, n, s);
+        walsh_step<3>(A, 0, K1, n, s);
         return hipGetLastError();
     }
     const size_t lds = size_t(2) * (n < 2 ? 2 : n) + size_t(8) * ((n + 31) / 32);

@@ -29,6 +29,14 @@ int main(int argc, char **argv) {
     E.lw_fold = lw;
     E.rowinfo = ri;
     for (uint32_t r = 0; r < n && r < rs::kEvalInlineRows; r += 3) E.erased[r >> 5] |= 1u << (r & 31);
+    if (n > rs::kEvalInlineRows) {  // past the inline bitmaps: per-row state bytes (bit 0 erased, bit 1 received)
+        std::vector<uint8_t> h(n);
+        for (uint32_t r = 0; r < n; ++r) h[r] = r % 3 == 0 ? 1 : 2;
+        uint8_t *st;
+        CK(hipMalloc(&st, n));
+        CK(hipMemcpy(st, h.data(), n, hipMemcpyHostToDevice));
+        E.state = st;
+    }
     for (int i = 0; i < 10; ++i) CK(rs::launch_eval_poly(E, 0));
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
@@ -40,6 +48,13 @@ int main(int argc, char **argv) {
     float ms;
     CK(hipEventElapsedTime(&ms, a, b));
     printf("eval_poly u=%u: %.2f us/launch back-to-back\n", u, ms * 1000 / 200);
+    {  // FNV-1a of the row info: compare across -D variants
+        std::vector<uint32_t> out(n);
+        CK(hipMemcpy(out.data(), ri, n * 4, hipMemcpyDeviceToHost));
+        uint64_t hsh = 0xcbf29ce484222325ull;
+        for (uint32_t v : out) hsh = (hsh ^ v) * 0x100000001b3ull;
+        printf("rowinfo hash %016llx\n", (unsigned long long)hsh);
+    }
     CK(hipDeviceSynchronize());
     CK(rs::launch_eval_poly(E, 0));
     CK(hipDeviceSynchronize());
