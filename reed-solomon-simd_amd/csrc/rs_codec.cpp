@@ -396,7 +396,14 @@ uint32_t g_max_k = 0;  // RS_MI355X_MAX_K (4..8) overrides the choice below
 // decodes with 6-bit levels (8192:8192 x 64 KiB 1 % / 100 %: 637 / 531 -> 840 / 641 GiB/s:
 // more levels below the top, so more of the FFT is pruned and more IFFT blocks skipped)
 uint32_t max_k_enc(uint32_t) { return g_max_k ? g_max_k : 8; }
-uint32_t max_k_dec() { return g_max_k ? g_max_k : 6; }
+// 2^13 work rows of short shards take two 7 + 6-bit levels instead of three
+// (5 + 4 + 4): two fewer launches.  4096:4096 x 1 KiB decode 46.1 / 43.2 ->
+// 40.4 / 38.5 us at 1 % / 100 % loss; at 2^14 and up 7-bit levels lost (8192:8192
+// x 1 KiB 70.3 -> 72.7 us, 1000:10000 49.5 -> 62.0 us; profiles/r04a/ab_maxk_shapes.txt)
+uint32_t max_k_dec(uint32_t u = 0, uint32_t packs = 0) {
+    if (g_max_k) return g_max_k;
+    return u == 13 && packs <= 512 ? 7 : 6;
+}
 struct Levels {
     uint32_t m = 0;
     uint32_t lo[4] = {0, 0, 0, 0}, K[4] = {0, 0, 0, 0};
@@ -841,7 +848,7 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
         launch_mono(rs::kMonoDecode, u, Mo, s, (received + missing) * uint64_t(g.packs) * 8 * g.stripes);
         return;
     }
-    if (!mono && nd <= rs::kPassEvalRows && levels(u, max_k_dec()).m == 1) {
+    if (!mono && nd <= rs::kPassEvalRows && levels(u, max_k_dec(u, g.packs)).m == 1) {
         // one launch: the single pass evaluates eval_poly itself (rs_kernels.hip
         // pass_eval_poly), the erasure state in its arguments
         rs::PassArgs A = base_args(ctx, g, nd);
@@ -861,7 +868,7 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
             A.ev_erased[r >> 5] |= uint32_t(st[r] == 1) << (r & 31);
             A.ev_received[r >> 5] |= uint32_t(st[r] == 2) << (r & 31);
         }
-        run_level(A, levels(u, max_k_dec()), 0, rs::kIfft | rs::kFft, nd, s, received, missing);
+        run_level(A, levels(u, max_k_dec(u, g.packs)), 0, rs::kIfft | rs::kFft, nd, s, received, missing);
         return;
     }
     uint32_t *d_rowinfo = static_cast<uint32_t *>(ws.rowinfo.get(size_t(nd) * 4));
@@ -903,7 +910,7 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
         launch_mono(rs::kMonoDecode, u, Mo, s, (received + missing) * uint64_t(g.packs) * 8);
         return;
     }
-    const Levels lv = levels(u, max_k_dec());
+    const Levels lv = levels(u, max_k_dec(u, g.packs));
     if (lv.m == 1) {
         A.src[0] = rec_map;
         A.src[1] = orig_map;
