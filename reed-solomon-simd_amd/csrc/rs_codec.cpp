@@ -197,8 +197,12 @@ struct rs_context {
     uint32_t mono_max_packs = 256;   // column kernel only up to this many packs (RS_MI355X_MONO_MAX_PACKS)
     // 2-element packs (rs_mono.hip Fmt<2>) for staged column-kernel decodes of at
     // most this many 4-element packs (RS_MI355X_E2_MAX_PACKS; 0 = never), and
-    // for encodes too when e2_encode (measured: tools/e2_probe.py)
-    uint32_t e2_max_packs = 192;
+    // for encodes too when e2_encode (measured: tools/e2_probe.py).
+    // Default: half the device's CUs, so the doubled workgroup count (one per
+    // 2-element pack) still runs in one wave of workgroups -- at 192 packs on 256
+    // CUs the 384 workgroups took two: 1024:1024 x 1536 B decode 26.3 -> 15.8 us
+    // with 4-element packs (profiles/r04a/e2_max_packs.txt)
+    uint32_t e2_max_packs = 128, e2_default = 128;
     bool e2_encode = false;
     int chunk_par = -1;           // RS_MI355X_CHUNK_PARALLEL: -1 by pack count (chunk_parallel), 0 / 1 forced
     uint32_t *d_lut2 = nullptr;   // perm2_by_log: the 2-element form of d_lut
@@ -1259,6 +1263,9 @@ rs_status rs_context_create(int device, rs_context **out) {
         check(hipMalloc(&ctx->d_lut2, T.perm2_by_log.size() * 4));
         check(hipMemcpy(ctx->d_lut2, T.perm2_by_log.data(), T.perm2_by_log.size() * 4, hipMemcpyHostToDevice));
         ctx->lw0 = T.log_walsh[0];
+        int cus = 0;
+        check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        ctx->e2_max_packs = ctx->e2_default = cus > 1 ? uint32_t(cus) / 2 : 1u;
         const char *nm = getenv("RS_MI355X_NO_MONO");
         ctx->mono = !(nm && nm[0] == '1');
         if (const char *mk = getenv("RS_MI355X_MAX_K")) {
@@ -2089,7 +2096,7 @@ rs_status rs_mono_enable(rs_context *ctx, int enable) {
     ctx->mono_all = (enable & 3) == 2;
     ctx->split = !(enable & 4);
     // + 8: 4-element packs only; + 16: 2-element packs wherever the staged kernel runs
-    ctx->e2_max_packs = (enable & 8) ? 0u : (enable & 16) ? 0xFFFFFFFFu : 192u;
+    ctx->e2_max_packs = (enable & 8) ? 0u : (enable & 16) ? 0xFFFFFFFFu : ctx->e2_default;
     ctx->e2_encode = (enable & 16) != 0;
     return RS_OK;
 }

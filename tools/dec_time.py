@@ -1,6 +1,7 @@
-"""Time one decode shape on the device (development aid): python tools/dec_time.py N M S [loss]
+"""Time one decode shape on the device (development aid): python tools/dec_time.py N M S [loss|enc]
 Prints the mean us per decode of `iters` back-to-back calls (1 % loss pattern of
-benches/benchmarks.rs:113-118 by default).  Environment knobs (RS_MI355X_*) apply."""
+benches/benchmarks.rs:113-118 by default; "enc": the encode instead).  Environment knobs
+(RS_MI355X_*) apply."""
 import os
 import sys
 import time
@@ -12,11 +13,23 @@ import torch  # noqa: E402
 import reed_solomon_simd as rs  # noqa: E402
 
 N, M, S = (int(a) for a in sys.argv[1:4])
-loss = float(sys.argv[4]) if len(sys.argv) > 4 else 0.01
+enc = len(sys.argv) > 4 and sys.argv[4] == "enc"
+loss = float(sys.argv[4]) if len(sys.argv) > 4 and not enc else 0.01
 iters = 50
 d_orig = torch.randint(0, 256, (N, S), dtype=torch.uint8, device="cuda")
 d_rec = torch.empty((M, S), dtype=torch.uint8, device="cuda")
 rs.encode_device(N, M, S, d_orig, d_rec)
+if enc:
+    call = rs.encode_device_call(N, M, S, d_orig, d_rec)
+    for _ in range(5):
+        call()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        call()
+    torch.cuda.synchronize()
+    print(f"{N}:{M}x{S} encode: {(time.perf_counter() - t0) / iters * 1e6:.2f} us")
+    sys.exit(0)
 L = max(1, -(-int(min(N, M) * loss * 100) // 100))
 op = np.ones(N, np.uint8)
 op[N - L:] = 0
