@@ -204,6 +204,7 @@ struct rs_context {
     // with 4-element packs (profiles/r04a/e2_max_packs.txt)
     uint32_t e2_max_packs = 128, e2_default = 128;
     bool e2_encode = false;
+    bool pad_small = true;        // decodes of 16..64 work rows on the 2^7-row column kernel (RS_MI355X_PAD_SMALL)
     int chunk_par = -1;           // RS_MI355X_CHUNK_PARALLEL: -1 by pack count (chunk_parallel), 0 / 1 forced
     uint32_t *d_lut2 = nullptr;   // perm2_by_log: the 2-element form of d_lut
     std::mutex img_mu;            // guards d_img, d_img2
@@ -792,7 +793,17 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
                 uint8_t *restored, hipStream_t s) {
     const uint32_t chunk = uint32_t(high ? next_pow2(M) : next_pow2(N));
     const uint32_t end = uint32_t(chunk + (high ? N : M));
-    const uint32_t nd = uint32_t(next_pow2(end)), u = ilog2(nd);
+    uint32_t nd = uint32_t(next_pow2(end)), u = ilog2(nd);
+    // Decodes of 16..64 work rows run the column kernel's smallest transform,
+    // 2^kMonoMinL rows: the rows past `end` are neither received nor erased
+    // (zero, as past 2^u), and any power of two >= end decodes the same bytes
+    // (eval_poly folds exactly onto it).  32:32 x 1 KiB decode
+    // 7.8 -> 6.0 us against the single fused pass; below 16 rows the pass is
+    // faster (1:1 4.8 vs 5.7 us; profiles/r04a/pad_small.txt).  RS_MI355X_PAD_SMALL=0: off
+    if (ctx->pad_small && nd >= 16 && nd < (1u << kMonoMinL) && ctx->mono && g.packs <= ctx->mono_max_packs) {
+        nd = 1u << kMonoMinL;
+        u = kMonoMinL;
+    }
     // erasure vector + received flags per work row
     std::vector<uint8_t> &st = ws.h_state;
     st.assign(nd, 0);
@@ -1266,6 +1277,8 @@ rs_status rs_context_create(int device, rs_context **out) {
         int cus = 0;
         check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         ctx->e2_max_packs = ctx->e2_default = cus > 1 ? uint32_t(cus) / 2 : 1u;
+        const char *psm = getenv("RS_MI355X_PAD_SMALL");
+        if (psm) ctx->pad_small = psm[0] == '1';
         const char *nm = getenv("RS_MI355X_NO_MONO");
         ctx->mono = !(nm && nm[0] == '1');
         if (const char *mk = getenv("RS_MI355X_MAX_K")) {

@@ -164,9 +164,10 @@ def test_eval_poly_forms_match_oracle(torch, rs, rate, N, M, u, S):
     assert np.array_equal(got[miss], orig[miss]) and np.array_equal(got[miss], want[miss])
 
 
-# decodes of at most 64 work rows: one pass that evaluates eval_poly itself
-# (rs_kernels.hip pass_eval_poly); (rate, N, M): work rows 2..64, both rates,
-# the LowRate end < n and the HighRate recovery padding
+# decodes of at most 64 work rows, one launch: 16..64 rows of shards up to 2 KiB on the
+# column kernel's 2^7-row transform (padded work rows), the others one pass that
+# evaluates eval_poly itself (rs_kernels.hip pass_eval_poly); (rate, N, M): work rows
+# 2..64, both rates, the LowRate end < n and the HighRate recovery padding
 SMALL_DEC = [("high", 1, 1), ("low", 1, 1), ("high", 3, 5), ("low", 5, 3), ("high", 2, 30), ("low", 30, 2),
              ("high", 32, 32), ("low", 32, 32), ("high", 31, 17), ("low", 17, 31), ("high", 40, 16),
              ("low", 16, 40), ("high", 1, 32), ("low", 32, 1)]
@@ -179,7 +180,7 @@ def _work_rows(rate, N, M):
 
 
 @pytest.mark.parametrize("rate,N,M", SMALL_DEC)
-@pytest.mark.parametrize("S", [64, 1024, 130])
+@pytest.mark.parametrize("S", [64, 1024, 130, 4096])
 def test_small_decode_is_one_fused_launch(torch, rs, rate, N, M, S):
     assert _work_rows(rate, N, M) <= 64
     rng = np.random.default_rng(N * 97 + M + S)
@@ -200,7 +201,11 @@ def test_small_decode_is_one_fused_launch(torch, rs, rate, N, M, S):
             rs.profile_enable(False)
         miss = op == 0
         assert np.array_equal(got[miss], orig[miss]) and np.array_equal(got[miss], want[miss]), (trial, L)
-        assert len(names) == 1 and names[0].startswith("k_pass<") and names[0].endswith(", 435>"), names
+        assert len(names) == 1, names
+        if _work_rows(rate, N, M) >= 16 and S <= 2048:
+            assert names[0].startswith("k_mono<7, "), names
+        else:
+            assert names[0].startswith("k_pass<") and names[0].endswith(", 435>"), names
 
 
 # ---------------------------------------------------------------------------
