@@ -323,10 +323,11 @@ rs_status rs_check_device(rs_context *ctx);
  * 2^11 / 2^12-row transforms (also: RS_MI355X_MONO_ALL=1).  Adding 4 turns off
  * the split decode plan of 2^9 .. 2^11-row decodes whose restored rows lie in
  * one half of the work rows (also: RS_MI355X_NO_SPLIT=1).  Single-chunk
- * decodes of at most 192 4-element packs use packs of 2 elements (twice the
- * workgroups; RS_MI355X_E2_MAX_PACKS sets the limit): adding 8 keeps 4-element
- * packs, adding 16 uses 2-element packs for every single-chunk launch, encodes
- * included.  A/B and tests; results are identical in every mode. */
+ * encodes and decodes of at most half the device's CU count of 4-element packs
+ * use packs of 2 elements (twice the workgroups; RS_MI355X_E2_MAX_PACKS sets
+ * the limit): adding 8 keeps 4-element packs, adding 16 uses 2-element packs
+ * for every single-chunk launch.  A/B and tests; results are identical in
+ * every mode. */
 rs_status rs_mono_enable(rs_context *ctx, int enable);
 
 /* ---- GF(2^16) tables (src/engine/tables.rs), host copies ---- */

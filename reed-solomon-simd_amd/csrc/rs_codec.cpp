@@ -203,7 +203,7 @@ struct rs_context {
     // CUs the 384 workgroups took two: 1024:1024 x 1536 B decode 26.3 -> 15.8 us
     // with 4-element packs (profiles/r04a/e2_max_packs.txt)
     uint32_t e2_max_packs = 128, e2_default = 128;
-    bool e2_encode = false;
+    bool e2_encode = true;
     bool pad_small = true;        // decodes of 16..64 work rows on the 2^7-row column kernel (RS_MI355X_PAD_SMALL)
     int chunk_par = -1;           // RS_MI355X_CHUNK_PARALLEL: -1 by pack count (chunk_parallel), 0 / 1 forced
     uint32_t *d_lut2 = nullptr;   // perm2_by_log: the 2-element form of d_lut
@@ -498,12 +498,13 @@ bool use_mono(rs_context *ctx, uint32_t L, const Geom &g, uint32_t chunks) {
     return ctx->mono_all || rs::mono_staged(int(L), chunks);
 }
 
-// Staged decodes of few packs use 2-element packs: twice the workgroups on
-// a chip whose CUs the 4-element packs leave idle (rs_mono.hip Fmt).  The
-// headline encode measured slower that way (9.4 vs 8.4 us per launch; after the
-// 20-word LDS slots and the slot swizzle of the 2-element tables about equal,
-// 8.5-8.8 vs 8.4-8.75 us), the decode faster (14.6 vs 15.4 us, now 13.8), hence
-// decodes only by default.
+// Staged transforms of few packs use 2-element packs: twice the workgroups on
+// a chip whose CUs the 4-element packs leave idle (rs_mono.hip Fmt).  Decodes
+// since round 2 (14.6 vs 15.4 us, now 13.8); encodes since round 4, when they
+// measured faster too (1024:1024 x 1 KiB 8.11 -> 7.96 us, 512:512 6.1 -> 5.7,
+// 1024:1024 x 256 B 8.0 -> 7.3; profiles/r04a/e2_encode_ab.txt) -- in rounds 2
+// and 3 the encode was slower (9.4 vs 8.4 us), then about equal (8.5-8.8 vs
+// 8.4-8.75 us).
 rs::MonoArgs mono_args(rs_context *ctx, uint32_t L, const Geom &g, bool staged, bool decode = false) {
     rs::MonoArgs M;
     const bool e2 = staged && (decode || ctx->e2_encode) && g.packs <= ctx->e2_max_packs && L <= 11;
@@ -2110,7 +2111,7 @@ rs_status rs_mono_enable(rs_context *ctx, int enable) {
     ctx->split = !(enable & 4);
     // + 8: 4-element packs only; + 16: 2-element packs wherever the staged kernel runs
     ctx->e2_max_packs = (enable & 8) ? 0u : (enable & 16) ? 0xFFFFFFFFu : ctx->e2_default;
-    ctx->e2_encode = (enable & 16) != 0;
+    ctx->e2_encode = !(enable & 8);
     return RS_OK;
 }
 
