@@ -507,7 +507,9 @@ bool use_mono(rs_context *ctx, uint32_t L, const Geom &g, uint32_t chunks) {
 // 8.4-8.75 us).
 rs::MonoArgs mono_args(rs_context *ctx, uint32_t L, const Geom &g, bool staged, bool decode = false) {
     rs::MonoArgs M;
-    const bool e2 = staged && (decode || ctx->e2_encode) && g.packs <= ctx->e2_max_packs && L <= 11;
+    // (a batch's stripes already fill the chip: the bound covers all its packs)
+    const bool e2 = staged && (decode || ctx->e2_encode) && uint64_t(g.packs) * g.stripes <= ctx->e2_max_packs &&
+                    L <= 11;
     M.elems = e2 ? 2 : 4;
     // 2-element packs: two per 4-element pack of the whole blocks, one per 2 tail elements
     M.packs = !e2 ? g.packs
