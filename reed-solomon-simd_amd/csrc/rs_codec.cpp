@@ -853,7 +853,9 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
             Mo.erased[r >> 5] |= uint32_t(st[r] == 1) << (r & 31);
             Mo.received[r >> 5] |= uint32_t(st[r] == 2) << (r & 31);
         }
-        if (ctx->split && rs::mono_split(int(u))) {
+        // (2^9 rows: the plain plan is faster, 256:256 x 1 KiB 8.3-8.8 -> 7.7 us;
+        // equal at 2^10, the split plan faster at 2^11: profiles/r04a/split_ab.txt)
+        if (ctx->split && rs::mono_split(int(u)) && u >= 10) {
             // split plan: every restored row in one half of the work rows
             bool lower = false, upper = false;
             for (uint32_t r = out_map.row_begin; r < out_map.row_end; ++r)
