@@ -894,7 +894,13 @@ hipError_t launch_pass(int K, int flags, const PassArgs &A, hipStream_t s) {
     // narrow slices when the wide shape's slices leave the chip under-filled
     const uint32_t wide_packs = K >= 8 ? 16 : K == 7 ? 32 : 64;
     const uint64_t wide_groups = uint64_t(A.nsets) * ((A.packs + wide_packs - 1) / wide_packs) * A.grid_chunks;
-    const bool narrow = wide_groups < 1024;
+// the narrow shape where the wide one would leave the chip under-filled: below
+// 1024 workgroups, 512 at K >= 7 (16384:16384 x 1 KiB encode 62.3 -> 53.2 us; the
+// K <= 6 passes lost with 512, profiles/r04a/pass_narrow_threshold.txt)
+#ifndef RS_PASS_NARROW_BELOW
+#define RS_PASS_NARROW_BELOW (K >= 7 ? 512 : 1024)
+#endif
+    const bool narrow = wide_groups < uint64_t(RS_PASS_NARROW_BELOW);
     switch (K) {
         case 0: return launch_shape<0>(narrow, flags, A, s);
         case 1: return launch_shape<1>(narrow, flags, A, s);
