@@ -10,12 +10,17 @@ same way and reported beside the headline value.
 
 --gpus N > 1: the parent process (which never touches the GPU) starts N ranks
 with torch.distributed.run, one process per GPU (RCCL = the "nccl" backend).
-The default workload at N > 1 is north_star's multi-GPU configuration,
-configs[4]: ONE 32768:32768 x 64 KiB stripe column-partitioned over the ranks
-(rank r encodes byte columns [r*S/N, (r+1)*S/N) of every shard) followed by an
-RCCL all-gather of the recovery slices over xGMI and a re-interleave; total
-work is fixed -> "scaling": "strong".  --config selects any other workload
-(the 1-GPU configs then run as independent stripes per rank: weak scaling).
+Every N reports the SAME primary workload: the headline stripe on every rank
+(independent stripes, no data-path collective; value = all ranks' bytes / the
+max-over-ranks time -> "scaling": "weak"), so the driver's 1/2/4/8 lines form one
+curve.  Beside it, the "sharded" sub-object carries north_star's multi-GPU
+configuration, configs[4], at the same N: ONE 32768:32768 x 64 KiB stripe
+column-partitioned over the ranks (rank r encodes byte columns [r*S/N, (r+1)*S/N)
+of every shard), an RCCL all-gather of the recovery slices over xGMI and a
+re-interleave -- total work fixed, strong scaling -- with its encode-only time,
+the all-gather cost, the per-GPU HBM fraction and a column-partitioned 1 % decode;
+its N = 1 point is in the --gpus 1 line.  --config 32768x32768x64k makes that
+workload the primary line instead (strong scaling).
 
 Timing: W untimed warmup steps, then exactly K steps bracketed by a barrier +
 torch.cuda.synchronize() on both sides, max over ranks.  Nothing else runs in
@@ -63,13 +68,15 @@ def parse():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--config", default=None, choices=sorted(CONFIGS),
-                   help=f"default: {HEADLINE} on 1 GPU, {SHARDED} (column-partitioned) on N > 1")
+                   help=f"default: {HEADLINE} (independent stripes per rank) at every N")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-copy", action="store_true", help="skip the 1 GiB device-copy context measurement")
     p.add_argument("--no-decode", action="store_true")
     p.add_argument("--no-host", action="store_true", help="skip the host-memory end-to-end measurement")
     p.add_argument("--no-object", action="store_true", help="skip the object-API (encoder/decoder) measurement")
+    p.add_argument("--no-sharded", action="store_true",
+                   help="skip the configs[4] strong-scaling sub-object (column partition + all-gather)")
     p.add_argument("--profile-steps", type=int, default=50)
     p.add_argument("--batch", type=int, default=64, help="stripes per call of the batched measurement (1 = skip)")
     p.add_argument("--plumbing", action="store_true",
@@ -158,7 +165,7 @@ def main():
     if args.shape_table:
         shape_table(args, rs, ctx, torch.device("cuda", local))
         return
-    config = args.config or (SHARDED if world > 1 else HEADLINE)
+    config = args.config or HEADLINE
     dev = torch.device("cuda", local)
     if config == SHARDED:
         sharded_bench(args, rs, ctx, world, rank, dev)
@@ -409,6 +416,11 @@ def stripe_bench(args, rs, ctx, config, world, rank, dev):
 
     copy_ref = None if args.no_copy else device_copy(dev)
 
+    # ---- configs[4] at the same N: strong scaling, column partition + RCCL all-gather ----
+    sharded = None
+    if config == HEADLINE and not args.no_sharded:
+        sharded = sharded_block(args, rs, ctx, world, rank, dev)
+
     # ---- CPU baseline (rank 0, N = 1 only) ----------------------------------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -429,6 +441,7 @@ def stripe_bench(args, rs, ctx, config, world, rank, dev):
             "host_e2e": host_e2e,
             "object_api": object_api,
             "roofline": roofline,
+            "sharded": sharded,
             "device_copy": copy_ref,
             "cpu_baseline": cpu,
         }
@@ -497,6 +510,68 @@ def device_copy(dev):
 
 # ---------------------------------------------------------------------------
 # configs[4]: one 32768:32768 x 64 KiB stripe column-partitioned over the ranks
+
+def sharded_block(args, rs, ctx, world, rank, dev):
+    """The "sharded" sub-object of every headline line: configs[4] at this N (strong scaling).
+    Rank r holds byte columns [r*w, (r+1)*w), w = 64 KiB / N, of the originals; `step` = its
+    encode in pieces + the RCCL all-gather of the recovery slices + the re-interleave
+    (ShardedEncoder), `encode_only` = the slice encode alone, both max over ranks; the
+    per-GPU roofline is the slice encode's.  `decode_1pct`: the reference's 1 % loss pattern
+    (benches/benchmarks.rs:113-138) decoded column-partitioned (ShardedDecoder: eval_poly on
+    every rank, slice decode, all-gather of the restored rows).  At N = 1 the step is the
+    single-device encode / decode (nothing to gather)."""
+    import torch
+
+    N, M, S = CONFIGS[SHARDED]
+    steps, warm = max(3, min(args.steps, 10)), 2
+    timed, _ = make_timer(world, dev)
+    stream = torch.cuda.current_stream(dev)  # collectives are ordered after this stream's kernels
+    w = S // world
+    g = torch.Generator(device=dev)
+    g.manual_seed(4321 + rank)
+    d_orig = torch.randint(0, 256, (N, w), dtype=torch.uint8, device=dev, generator=g)  # this rank's columns
+    d_rec = torch.empty((M, S), dtype=torch.uint8, device=dev)
+    enc = rs.ShardedEncoder(N, M, S, device=dev, stream=stream, ctx=ctx) if world > 1 else None
+    part = enc.part if world > 1 else d_rec
+    compute = rs.encode_device_call(N, M, w, d_orig, part, stream=stream, ctx=ctx)
+    t_comp = timed(compute, steps, warm) / steps
+    t_step = timed(lambda: enc(d_orig, d_rec), steps, warm) / steps if world > 1 else t_comp
+    per_gpu = (N + M) * w
+    rl = roofline_of(rs, ctx, compute, 3, per_gpu, SHARDED)
+    total = (N + M) * S
+    out = {"config": f"{N}:{M} x {S} B (configs[4]), column slice of {w} B per GPU",
+           "n_gpus": world, "scaling": "strong", "steps": steps,
+           "step_ms": round(t_step * 1e3, 4), "GiBps": round(total / t_step / 2**30, 3),
+           "encode_only": {"ms_per_step": round(t_comp * 1e3, 4), "GiBps": round(total / t_comp / 2**30, 3)},
+           "allgather_and_interleave_ms": round((t_step - t_comp) * 1e3, 4),
+           "pipeline_pieces": enc.chunks if world > 1 else 1,
+           "per_gpu_roofline": {k: rl[k] for k in ("kernel", "achieved", "frac", "traffic", "valu_frac")},
+           "parallelism": f"column partition x{world}" + (" + all_gather_into_tensor (RCCL)" if world > 1 else "")}
+    del enc
+    # column-partitioned decode at 1 % loss: every rank restores the lost originals' full rows
+    L = -(-min(N, M) // 100)
+    op = rs.present_mask([1] * (N - L) + [0] * L)
+    rp = rs.present_mask([1] * L + [0] * (M - L))
+    rec_cols = part if world > 1 else d_rec  # this rank's recovery columns (its own encode above)
+    d_x = torch.empty((N, S), dtype=torch.uint8, device=dev)
+    if world > 1:
+        dec = rs.ShardedDecoder(N, M, S, device=dev, stream=stream, ctx=ctx)
+        x_cols = torch.empty((N, w), dtype=torch.uint8, device=dev)
+        dcomp = rs.decode_device_call(N, M, w, d_orig, op, rec_cols, rp, x_cols, stream=stream, ctx=ctx)
+        td_comp = timed(dcomp, steps, warm) / steps
+        td_step = timed(lambda: dec(d_orig, op, rec_cols, rp, d_x), steps, warm) / steps
+        del dec, x_cols
+    else:
+        dcomp = rs.decode_device_call(N, M, w, d_orig, op, rec_cols, rp, d_x, stream=stream, ctx=ctx)
+        td_comp = td_step = timed(dcomp, steps, warm) / steps
+    out["decode_1pct"] = {"step_ms": round(td_step * 1e3, 4), "GiBps": round(total / td_step / 2**30, 3),
+                          "decode_only_ms": round(td_comp * 1e3, 4),
+                          "decode_only_GiBps": round(total / td_comp / 2**30, 3),
+                          "restored_rows": L}
+    del d_orig, d_rec, d_x
+    torch.cuda.empty_cache()
+    return out
+
 
 def sharded_bench(args, rs, ctx, world, rank, dev):
     """SURVEY.md 8(e), DESIGN.md "Multi-GPU": rank r encodes byte columns [r*w, (r+1)*w),

@@ -285,6 +285,15 @@ struct rs_context {
         }
     };
     Pipe *pipe = nullptr;
+    // one-shot rs_encode / rs_decode (lib.rs:251-353): the working space of the last calls
+    // (pinned staging, device buffers, workspace, stream), handed to the next call's
+    // encoder / decoder as an EncoderWork / DecoderWork would be -- no hipHostMalloc,
+    // hipMalloc or hipStreamCreate per call, and no hipHostFree / hipFree, which
+    // synchronize the device.  At most kOneShotPool of each, freed with the context.
+    static constexpr size_t kOneShotPool = 2;
+    std::mutex pool_mu;
+    std::vector<rs_encoder_work *> enc_pool;
+    std::vector<rs_decoder_work *> dec_pool;
     bool prof = false;
     struct Rec {
         hipEvent_t a, b;
@@ -1295,7 +1304,8 @@ rs_status rs_context_create(int device, rs_context **out) {
         const char *ma = getenv("RS_MI355X_MONO_ALL");
         ctx->mono_all = ma && ma[0] == '1';
         if (const char *mp = getenv("RS_MI355X_MONO_MAX_PACKS")) ctx->mono_max_packs = uint32_t(strtoul(mp, nullptr, 10));
-        if (const char *e2 = getenv("RS_MI355X_E2_MAX_PACKS")) ctx->e2_max_packs = uint32_t(strtoul(e2, nullptr, 10));
+        if (const char *e2 = getenv("RS_MI355X_E2_MAX_PACKS"))  // also what rs_mono_enable resets to
+            ctx->e2_max_packs = ctx->e2_default = uint32_t(strtoul(e2, nullptr, 10));
         if (const char *cp = getenv("RS_MI355X_CHUNK_PARALLEL"))  // "0" / "1"; anything else: automatic
             ctx->chunk_par = cp[0] == '1' && !cp[1] ? 1 : cp[0] == '0' && !cp[1] ? 0 : -1;
         // column-kernel twiddle images of every transform size, built now: a lazy
@@ -1315,6 +1325,8 @@ rs_status rs_context_create(int device, rs_context **out) {
 
 void rs_context_destroy(rs_context *ctx) {
     if (!ctx) return;
+    for (rs_encoder_work *w : ctx->enc_pool) rs_encoder_work_free(w);
+    for (rs_decoder_work *w : ctx->dec_pool) rs_decoder_work_free(w);
     delete ctx->pipe;
     if (ctx->d_tw) (void)hipFree(ctx->d_tw);
     if (ctx->d_lut) (void)hipFree(ctx->d_lut);
@@ -1453,9 +1465,27 @@ uint64_t slice_width(uint64_t S, uint32_t slices) {
     return std::max<uint64_t>(64, (blocks + k - 1) / k * 64);  // S < 64: one slice (the tail)
 }
 
-// hipMemcpy2DAsync of the rows [r0, r1) where flag[r] == want, in runs
+// hipMemcpy2DAsync of the rows [r0, r1) where flag[r] == want, in runs.  With
+// `span_ok` (the destination's other rows are scratch nobody reads), more than
+// kCopyRuns runs go as one copy of the span from the first to the last wanted row:
+// every copy costs ~10 us of latency, so scattered losses (hundreds of runs) would
+// otherwise cost more than the bytes they skip.
+constexpr uint64_t kCopyRuns = 4;
 void copy_rows(uint8_t *dst, const uint8_t *src, uint64_t pitch, uint64_t width, const uint8_t *flag, uint8_t want,
-               uint64_t rows, hipMemcpyKind kind, hipStream_t s) {
+               uint64_t rows, hipMemcpyKind kind, hipStream_t s, bool span_ok = false) {
+    if (flag && span_ok) {
+        uint64_t runs = 0, first = rows, last = 0;
+        for (uint64_t i = 0; i < rows; ++i)
+            if ((flag[i] != 0) == (want != 0)) {
+                runs += i == 0 || (flag[i - 1] != 0) != (want != 0);
+                first = std::min(first, i);
+                last = i;
+            }
+        if (runs > kCopyRuns) {
+            copy_rows(dst + first * pitch, src + first * pitch, pitch, width, nullptr, 1, last + 1 - first, kind, s);
+            return;
+        }
+    }
     uint64_t r = 0;
     while (r < rows) {
         if (flag && (flag[r] != 0) != (want != 0)) {
@@ -1551,8 +1581,9 @@ rs_status rs_decode_host(rs_context *ctx, rs_rate rate, uint64_t N, uint64_t M, 
             hipStream_t s = P.st[k % rs_context::Pipe::kStreams];
             Workspace &ws = P.ws[k % rs_context::Pipe::kStreams];
             // only received rows travel in, only restored rows travel out
-            copy_rows(d_o + a, h_o + a, S, b - a, orig_present, 1, N, hipMemcpyHostToDevice, s);
-            copy_rows(d_r + a, h_r + a, S, b - a, rec_present, 1, M, hipMemcpyHostToDevice, s);
+            // (absent rows of the device staging are scratch; the caller's h_restored is not)
+            copy_rows(d_o + a, h_o + a, S, b - a, orig_present, 1, N, hipMemcpyHostToDevice, s, true);
+            copy_rows(d_r + a, h_r + a, S, b - a, rec_present, 1, M, hipMemcpyHostToDevice, s, true);
             const Geom g = device_geom(b - a, S, S, S, {d_o + a, d_r + a, d_x + a});
             decode_dev(ctx, ws, high, g, N, M, d_o + a, orig_present, d_r + a, rec_present, d_x + a, s);
             copy_rows(h_x + a, d_x + a, S, b - a, orig_present, 0, N, hipMemcpyDeviceToHost, s);
@@ -1848,11 +1879,12 @@ rs_status rs_decoder_decode(rs_decoder *d, rs_error *err) {
         auto *d_rec = static_cast<uint8_t *>(d->d_rec.get(d->M * row));
         auto *d_out = static_cast<uint8_t *>(d->d_out.get(d->N * row));
         uint8_t *h_out = d->h_out.get(d->N * row);
-        copy_rows(d_orig, d->h_orig.p, row, row, d->orig_present.data(), 1, d->N, hipMemcpyHostToDevice, s);
-        copy_rows(d_rec, d->h_rec.p, row, row, d->rec_present.data(), 1, d->M, hipMemcpyHostToDevice, s);
+        // (absent rows of the device buffers and of h_out are scratch: copied runs may span them)
+        copy_rows(d_orig, d->h_orig.p, row, row, d->orig_present.data(), 1, d->N, hipMemcpyHostToDevice, s, true);
+        copy_rows(d_rec, d->h_rec.p, row, row, d->rec_present.data(), 1, d->M, hipMemcpyHostToDevice, s, true);
         decode_dev(d->ctx, d->ws, d->high, g, d->N, d->M, d_orig, d->orig_present.data(), d_rec,
                    d->rec_present.data(), d_out, s);
-        copy_rows(h_out, d_out, row, row, d->orig_present.data(), 0, d->N, hipMemcpyDeviceToHost, s);
+        copy_rows(h_out, d_out, row, row, d->orig_present.data(), 0, d->N, hipMemcpyDeviceToHost, s, true);
         check(hipStreamSynchronize(s));
         if (d->S != row) {  // tails: the reference's unpadded shards (shards.rs:62-74)
             d->h_tail.resize(d->N * d->S);
@@ -1896,6 +1928,31 @@ void rs_decoder_work_free(rs_decoder_work *w) { delete w; }
 
 // ---- one-shot (lib.rs:251-353) -------------------------------------------------
 
+}  // extern "C"
+namespace {
+template <typename W>
+W *pool_take(rs_context *ctx, std::vector<W *> &pool) {
+    std::lock_guard<std::mutex> lock(ctx->pool_mu);
+    if (pool.empty()) return nullptr;
+    W *w = pool.back();
+    pool.pop_back();
+    return w;
+}
+template <typename W>
+void pool_put(rs_context *ctx, std::vector<W *> &pool, W *w) {
+    if (!w) return;
+    {
+        std::lock_guard<std::mutex> lock(ctx->pool_mu);
+        if (pool.size() < rs_context::kOneShotPool) {
+            pool.push_back(w);
+            return;
+        }
+    }
+    delete w;
+}
+}  // namespace
+extern "C" {
+
 rs_status rs_encode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const uint8_t *const *original,
                     uint64_t given, uint8_t *recovery_out, rs_error *err) {
     if (!ctx) return set_err(err, RS_ERR_INVALID_ARGUMENT);
@@ -1911,13 +1968,15 @@ rs_status rs_encode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const u
     }
     (void)S;  // shard size is inferred from the first shard, as the reference does; S = its length
     rs_encoder *e = nullptr;
-    rs_status st = rs_encoder_new(ctx, RS_RATE_DEFAULT, N, M, S, &e, err);
+    rs_status st = rs_encoder_new_with_work(ctx, RS_RATE_DEFAULT, N, M, S, pool_take(ctx, ctx->enc_pool), &e, err);
     if (st != RS_OK) return st;
     for (uint64_t i = 0; i < given && st == RS_OK; ++i) st = rs_encoder_add_original_shard(e, original[i], S, err);
     if (st == RS_OK) st = rs_encoder_encode(e, err);
     if (st == RS_OK && recovery_out)
         for (uint64_t i = 0; i < M; ++i) std::memcpy(recovery_out + i * S, rs_encoder_recovery(e, i), S);
-    rs_encoder_free(e);
+    rs_encoder_work *w = nullptr;
+    rs_encoder_into_parts(e, nullptr, &w);
+    pool_put(ctx, ctx->enc_pool, w);
     return st;
 }
 
@@ -1939,7 +1998,7 @@ rs_status rs_decode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const u
         return RS_ERR_NOT_ENOUGH_SHARDS;
     }
     rs_decoder *d = nullptr;
-    rs_status st = rs_decoder_new(ctx, RS_RATE_DEFAULT, N, M, S, &d, err);
+    rs_status st = rs_decoder_new_with_work(ctx, RS_RATE_DEFAULT, N, M, S, pool_take(ctx, ctx->dec_pool), &d, err);
     if (st != RS_OK) return st;
     // shard lengths are S by construction of this C entry point; per-shard
     // lengths are checked by the Python / C++ front-ends that know them
@@ -1954,7 +2013,9 @@ rs_status rs_decode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const u
                 if (restored_out) std::memcpy(restored_out + i * S, rs_decoder_restored_original(d, i), S);
                 if (restored_mask) restored_mask[i] = 1;
             }
-    rs_decoder_free(d);
+    rs_decoder_work *w = nullptr;
+    rs_decoder_into_parts(d, nullptr, &w);
+    pool_put(ctx, ctx->dec_pool, w);
     return st;
 }
 

@@ -622,6 +622,12 @@ for _name, _r in (("Default", RATE_DEFAULT), ("High", RATE_HIGH), ("Low", RATE_L
 
 # ---------------------------------------------------------------------------
 # one-shot (src/lib.rs:251-353)
+#
+# Each call builds an encoder / decoder as the reference does, on the working space
+# the previous one-shot call left (into_parts -> work=): pinned staging, device
+# buffers and stream are reused, so a call allocates (and frees) nothing when the
+# shapes repeat -- a hipHostFree or hipFree per call would synchronize the device.
+_oneshot_work: Dict[str, _Work] = {}
 
 def encode(original_count: int, recovery_count: int, original: Iterable) -> List[bytes]:
     if not ReedSolomonEncoder.supports(original_count, recovery_count):
@@ -631,13 +637,16 @@ def encode(original_count: int, recovery_count: int, original: Iterable) -> List
         first = bytes(next(it))
     except StopIteration:
         raise TooFewOriginalShards(original_count=original_count, original_received_count=0) from None
-    enc = ReedSolomonEncoder(original_count, recovery_count, len(first))
-    enc.add_original_shard(first)
-    for s in it:
-        enc.add_original_shard(s)
-    res = enc.encode()
-    out = list(res.recovery_iter())
-    res.drop()
+    enc = ReedSolomonEncoder(original_count, recovery_count, len(first), work=_oneshot_work.pop("enc", None))
+    try:
+        enc.add_original_shard(first)
+        for s in it:
+            enc.add_original_shard(s)
+        res = enc.encode()
+        out = list(res.recovery_iter())
+        res.drop()
+    finally:
+        _oneshot_work["enc"] = enc.into_parts()[1]
     return out
 
 
@@ -655,15 +664,18 @@ def decode(original_count: int, recovery_count: int, original: Iterable[Tuple[in
         raise NotEnoughShards(original_count=original_count, original_received_count=len(original),
                               recovery_received_count=0) from None
     shard_bytes = len(bytes(first[1]))
-    dec = ReedSolomonDecoder(original_count, recovery_count, shard_bytes)
-    for i, s in original:
-        dec.add_original_shard(i, s)
-    dec.add_recovery_shard(first[0], first[1])
-    for i, s in rit:
-        dec.add_recovery_shard(i, s)
-    res = dec.decode()
-    out = dict(res.restored_original_iter())
-    res.drop()
+    dec = ReedSolomonDecoder(original_count, recovery_count, shard_bytes, work=_oneshot_work.pop("dec", None))
+    try:
+        for i, s in original:
+            dec.add_original_shard(i, s)
+        dec.add_recovery_shard(first[0], first[1])
+        for i, s in rit:
+            dec.add_recovery_shard(i, s)
+        res = dec.decode()
+        out = dict(res.restored_original_iter())
+        res.drop()
+    finally:
+        _oneshot_work["dec"] = dec.into_parts()[1]
     return out
 
 
@@ -913,25 +925,21 @@ def decode_host(original_count: int, recovery_count: int, shard_bytes: int, h_or
                                ctypes.byref(err)), err)
 
 
-class ShardedEncoder:
-    """Column-partitioned encode of ONE stripe over the ranks of a process group, one GPU per
-    rank.  Rank r owns byte columns [r*w, (r+1)*w) of every shard,
-    w = shard_bytes / world (whole 64-byte blocks); it encodes them on its device
-    (rs_encode_device_strided) into a [recovery_count x w] slice, and an all-gather (RCCL over
-    xGMI for the "nccl" backend) plus a re-interleave assembles the whole [recovery_count x
-    shard_bytes] recovery matrix on every rank.  Every engine op is column-wise, so the result
-    equals a single-device encode.
+class _ColumnSplit:
+    """Shared plumbing of the column-partitioned encode and decode of ONE stripe over the ranks
+    of a process group, one GPU per rank.  Rank r owns byte
+    columns [r*w, (r+1)*w) of every shard, w = shard_bytes / world (whole 64-byte blocks).
+    Every engine op is column-wise (src/engine/utils.rs:35-43, src/engine/engine_naive.rs:107-146),
+    so a rank's slice is coded on its own device with no exchange, and the all-gathered slices
+    equal the single-device result.
 
-    Pipelined (`chunks` > 1): the slice is encoded in `chunks` column pieces; piece c's
-    all-gather (asynchronous, on the collective's own stream) runs while piece c+1 is encoded
-    and piece c-1 is re-interleaved, so the link-bound all-gather hides the encode and the
-    interleave copies.  Buffers are allocated once per encoder.  `encode_slice(orig_cols,
-    rec_slice)` replaces the per-piece device encode (tests drive this plumbing on CPU with a
-    stand-in)."""
+    The slice is coded in `chunks` column pieces: piece c's all-gather (asynchronous, on the
+    collective's own stream for RCCL) runs while piece c+1 is coded and piece c-1 is
+    re-interleaved.  `force_collective` keeps that path at world 1 (the all-gather of one rank
+    is a copy through the backend), so RCCL's stream ordering is exercised on one GPU."""
 
-    def __init__(self, original_count: int, recovery_count: int, shard_bytes: int, device=None, group=None,
-                 stream=None, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None, encode_slice=None,
-                 chunks: Optional[int] = None):
+    def __init__(self, original_count, recovery_count, shard_bytes, device, group, stream, rate_, ctx, chunks,
+                 force_collective):
         import torch
         import torch.distributed as dist
 
@@ -942,42 +950,92 @@ class ShardedEncoder:
                              f"{self.world} ranks")
         self.N, self.M, self.S = original_count, recovery_count, shard_bytes
         self.w = shard_bytes // self.world
+        self.collective = self.world > 1 or bool(force_collective)
         if chunks is None:  # pieces of at least 2 KiB of columns, at most 4
             chunks = max(c for c in (1, 2, 4) if self.w % (64 * c) == 0 and (c == 1 or self.w // c >= 2048))
         if chunks < 1 or self.w % (64 * chunks):
             raise ValueError(f"{chunks} pieces do not split a {self.w}-byte column slice into whole 64-byte blocks")
         self.chunks, self.cw = chunks, self.w // chunks
         self.stream, self.rate, self.ctx = stream, rate_, ctx
-        self._encode_slice = encode_slice
         self.nccl = dist.get_backend(group) == "nccl"
-        dev = torch.device(device) if device is not None else (
+        self.dev = torch.device(device) if device is not None else (
             torch.device("cuda", torch.cuda.current_device()) if self.nccl else torch.device("cpu"))
-        self.part = torch.empty((recovery_count, self.w), dtype=torch.uint8, device=dev)
-        self.pieces = ([torch.empty((recovery_count, self.cw), dtype=torch.uint8, device=dev)
-                        for _ in range(chunks)] if self.world > 1 else [])
-        self.gathered = ([torch.empty((self.world, recovery_count, self.cw), dtype=torch.uint8, device=dev)
-                          for _ in range(chunks)] if self.world > 1 else [])
 
-    def columns(self, d_original):
-        """This rank's column slice of a full [N x S] original matrix (a strided view)."""
-        return d_original[:, self.rank * self.w:(self.rank + 1) * self.w]
+    def columns(self, d_matrix):
+        """This rank's column slice of a full [rows x S] shard matrix (a strided view)."""
+        return d_matrix[:, self.rank * self.w:(self.rank + 1) * self.w]
+
+    def _piece(self, c):
+        return slice(c * self.cw, (c + 1) * self.cw)
+
+    def _on_stream(self, call) -> None:
+        """Run a device call on the caller-supplied stream, ordered against the current one:
+        the call waits for what the current stream has queued (the writes of its inputs and,
+        through the previous call's work.wait(), the all-gathers still reading its output),
+        and the collectives, which follow the current stream, wait for the call."""
+        if self.stream is None:
+            call(None)
+            return
+        import torch
+        cur = torch.cuda.current_stream()
+        self.stream.wait_stream(cur)
+        call(self.stream)
+        cur.wait_stream(self.stream)
+
+    def _all_gather(self, out, inp):
+        import torch.distributed as dist
+
+        if self.nccl:
+            return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True)
+        return dist.all_gather(list(out.unbind(0)), inp, group=self.group, async_op=True)
+
+    def _pipeline(self, code, start, finish) -> None:
+        pending = None
+        for c in range(self.chunks):
+            code(c)
+            work = start(c)
+            if pending is not None:  # piece c-1's interleave behind piece c's coding
+                finish(*pending)
+            pending = (c, work)
+        finish(*pending)
+
+
+class ShardedEncoder(_ColumnSplit):
+    """Column-partitioned encode of ONE stripe (_ColumnSplit): rank r encodes its [N x w]
+    columns (rs_encode_device_strided) into [M x w] recovery slices, and an all-gather (RCCL
+    over xGMI for the "nccl" backend) plus a re-interleave assembles the whole [M x S] recovery
+    matrix on every rank.  `encode_slice(orig_cols, rec_slice)` replaces the per-piece device
+    encode (tests drive the plumbing on CPU with a stand-in)."""
+
+    def __init__(self, original_count: int, recovery_count: int, shard_bytes: int, device=None, group=None,
+                 stream=None, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None, encode_slice=None,
+                 chunks: Optional[int] = None, force_collective: bool = False):
+        import torch
+
+        super().__init__(original_count, recovery_count, shard_bytes, device, group, stream, rate_, ctx, chunks,
+                         force_collective)
+        self._encode_slice = encode_slice
+        M, dev = recovery_count, self.dev
+        self._part = None
+        self.pieces = ([torch.empty((M, self.cw), dtype=torch.uint8, device=dev) for _ in range(self.chunks)]
+                       if self.collective else [])
+        self.gathered = ([torch.empty((self.world, M, self.cw), dtype=torch.uint8, device=dev)
+                          for _ in range(self.chunks)] if self.collective else [])
 
     def _encode(self, cols, out) -> None:
         if self._encode_slice is not None:
             self._encode_slice(cols, out)
             return
-        if self.stream is None:
-            encode_device(self.N, self.M, cols.shape[1], cols, out, rate_=self.rate, ctx=self.ctx)
-            return
-        import torch
-        cur = torch.cuda.current_stream()
-        # a caller-supplied stream: the encode waits for what the current stream has
-        # queued -- the writes of `cols`, and (through the previous call's work.wait())
-        # the all-gathers still reading `out` = pieces[c] -- and the collectives, which
-        # follow the current stream, wait for the encode
-        self.stream.wait_stream(cur)
-        encode_device(self.N, self.M, cols.shape[1], cols, out, stream=self.stream, rate_=self.rate, ctx=self.ctx)
-        cur.wait_stream(self.stream)
+        self._on_stream(lambda s: encode_device(self.N, self.M, cols.shape[1], cols, out, stream=s, rate_=self.rate,
+                                                ctx=self.ctx))
+
+    @property
+    def part(self):
+        """This rank's [M x w] recovery slice (encode_local / gather; allocated on first use)."""
+        if self._part is None:
+            import torch
+            self._part = torch.empty((self.M, self.w), dtype=torch.uint8, device=self.dev)
+        return self._part
 
     def encode_local(self, orig_cols) -> None:
         """Encode this rank's [N x w] columns into self.part (one device call)."""
@@ -985,46 +1043,118 @@ class ShardedEncoder:
 
     def gather(self, d_recovery) -> None:
         """All-gather every rank's self.part and re-interleave into d_recovery [M x S]."""
-        if self.world == 1:
+        if not self.collective:
             d_recovery.copy_(self.part)
             return
         for c in range(self.chunks):
-            self.pieces[c].copy_(self.part[:, c * self.cw:(c + 1) * self.cw])
-        self._gather_pieces(d_recovery, range(self.chunks))
+            self.pieces[c].copy_(self.part[:, self._piece(c)])
+        works = [(c, self._start_gather(c)) for c in range(self.chunks)]
+        for c, work in works:
+            self._finish_gather(c, work, d_recovery)
 
     def _start_gather(self, c):
-        import torch.distributed as dist
+        return self._all_gather(self.gathered[c], self.pieces[c])
 
-        if self.nccl:
-            return dist.all_gather_into_tensor(self.gathered[c], self.pieces[c], group=self.group, async_op=True)
-        return dist.all_gather(list(self.gathered[c].unbind(0)), self.pieces[c], group=self.group, async_op=True)
-
-    def _finish_gather(self, work, c, d_recovery) -> None:
+    def _finish_gather(self, c, work, d_recovery) -> None:
         work.wait()  # (nccl: the current stream waits for the collective's stream)
-        out = d_recovery.view(self.M, self.world, self.w)[:, :, c * self.cw:(c + 1) * self.cw]
+        out = d_recovery.view(self.M, self.world, self.w)[:, :, self._piece(c)]
         out.copy_(self.gathered[c].permute(1, 0, 2))
-
-    def _gather_pieces(self, d_recovery, pieces) -> None:
-        works = [(c, self._start_gather(c)) for c in pieces]
-        for c, work in works:
-            self._finish_gather(work, c, d_recovery)
 
     def __call__(self, orig_cols, d_recovery) -> None:
         """Encode this rank's [N x w] columns and assemble d_recovery [M x S] on every rank."""
-        if self.world == 1:
+        if not self.collective:
             self._encode(orig_cols, d_recovery)
             return
-        pending = None
-        for c in range(self.chunks):
-            self._encode(orig_cols[:, c * self.cw:(c + 1) * self.cw], self.pieces[c])
-            work = self._start_gather(c)
-            if pending is not None:  # piece c-1's interleave behind piece c's encode
-                self._finish_gather(pending[1], pending[0], d_recovery)
-            pending = (c, work)
-        self._finish_gather(pending[1], pending[0], d_recovery)
+        self._pipeline(lambda c: self._encode(orig_cols[:, self._piece(c)], self.pieces[c]), self._start_gather,
+                       lambda c, work: self._finish_gather(c, work, d_recovery))
 
 
-_sharded_cache: Dict[tuple, ShardedEncoder] = {}
+class ShardedDecoder(_ColumnSplit):
+    """Column-partitioned decode of ONE stripe (_ColumnSplit).  The erasure
+    pattern is the same on every rank, so eval_poly (src/rate/rate_high.rs:186-204) is
+    replicated: each rank decodes its [N x w] / [M x w] column slices
+    (rs_decode_device_strided, src/rate/rate_high.rs:172-254 per column) into a slice buffer,
+    packs the restored (= missing original) rows of each piece, and an all-gather plus a
+    re-interleave writes the missing originals' full rows into d_restored [N x S] on every
+    rank; present rows of d_restored are never written, as in the single-device decode.
+    `decode_slice(orig_cols, original_present, rec_cols, recovery_present, out)` replaces the
+    per-piece device decode (CPU tests)."""
+
+    def __init__(self, original_count: int, recovery_count: int, shard_bytes: int, device=None, group=None,
+                 stream=None, rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None, decode_slice=None,
+                 chunks: Optional[int] = None, force_collective: bool = False):
+        import torch
+
+        super().__init__(original_count, recovery_count, shard_bytes, device, group, stream, rate_, ctx, chunks,
+                         force_collective)
+        self._decode_slice = decode_slice
+        self.part = (torch.empty((original_count, self.w), dtype=torch.uint8, device=self.dev)
+                     if self.collective else None)
+        self._pattern = None  # (original mask, missing-row index, packed pieces, gathered pieces)
+
+    def _prepare(self, op: bytes):
+        """Missing-row index and gather buffers of one erasure pattern (kept while it repeats)."""
+        if self._pattern is not None and self._pattern[0] == op:
+            return self._pattern
+        import numpy as np
+        import torch
+
+        miss = np.flatnonzero(np.frombuffer(op, dtype=np.uint8) == 0).astype(np.int64)
+        L, dev = len(miss), self.dev
+        idx = torch.from_numpy(miss).to(dev)
+        packed = [torch.empty((L, self.cw), dtype=torch.uint8, device=dev) for _ in range(self.chunks)]
+        gathered = [torch.empty((self.world, L, self.cw), dtype=torch.uint8, device=dev) for _ in range(self.chunks)]
+        self._pattern = (op, idx, packed, gathered)
+        return self._pattern
+
+    def _decode(self, orig_cols, op, rec_cols, rp, out) -> None:
+        if self._decode_slice is not None:
+            self._decode_slice(orig_cols, op, rec_cols, rp, out)
+            return
+        self._on_stream(lambda s: decode_device(self.N, self.M, out.shape[1], orig_cols, op, rec_cols, rp, out,
+                                                stream=s, rate_=self.rate, ctx=self.ctx))
+
+    def __call__(self, orig_cols, original_present, rec_cols, recovery_present, d_restored) -> None:
+        """Decode this rank's column slices (orig_cols [N x w], rec_cols [M x w]; rows not
+        present are ignored) and write every missing original's full row of d_restored
+        [N x S] on every rank."""
+        import torch
+
+        op = _check_mask(present_mask(original_present), self.N, "original_present")
+        rp = _check_mask(present_mask(recovery_present), self.M, "recovery_present")
+        if not self.collective:
+            self._decode(orig_cols, op, rec_cols, rp, d_restored)
+            return
+        _, idx, packed, gathered = self._prepare(op)
+        if idx.numel() == 0:  # nothing to restore (decoder_work.rs:131-132); the call still validates
+            self._decode(orig_cols[:, self._piece(0)], op, rec_cols[:, self._piece(0)], rp,
+                         self.part[:, self._piece(0)])
+            return
+
+        def code(c):
+            sl = self._piece(c)
+            self._decode(orig_cols[:, sl], op, rec_cols[:, sl], rp, self.part[:, sl])
+            torch.index_select(self.part[:, sl], 0, idx, out=packed[c])
+
+        def finish(c, work):
+            work.wait()
+            out = d_restored.view(self.N, self.world, self.w)[:, :, self._piece(c)]
+            out.index_copy_(0, idx, gathered[c].permute(1, 0, 2))
+
+        self._pipeline(code, lambda c: self._all_gather(gathered[c], packed[c]), finish)
+
+
+_sharded_cache: Dict[tuple, _ColumnSplit] = {}
+
+
+def _sharded(cls, original_count, recovery_count, shard_bytes, device, group, stream, rate_, ctx):
+    key = (cls.__name__, original_count, recovery_count, shard_bytes, id(group), str(device), _stream(stream), rate_,
+           id(ctx))
+    obj = _sharded_cache.get(key)
+    if obj is None:
+        obj = _sharded_cache[key] = cls(original_count, recovery_count, shard_bytes, device=device, group=group,
+                                        stream=stream, rate_=rate_, ctx=ctx)
+    return obj
 
 
 def encode_device_sharded(original_count: int, recovery_count: int, shard_bytes: int, d_original, d_recovery,
@@ -1032,16 +1162,26 @@ def encode_device_sharded(original_count: int, recovery_count: int, shard_bytes:
     """Multi-GPU encode of one large stripe: each rank (one GPU each) encodes its column slice of
     d_original [N x S] on its device, then an all-gather assembles d_recovery [M x S] everywhere
     (ShardedEncoder, cached per shape / group / device)."""
-    key = (original_count, recovery_count, shard_bytes, id(group), str(d_recovery.device), _stream(stream), rate_,
-           id(ctx))
-    enc = _sharded_cache.get(key)
-    if enc is None:
-        enc = _sharded_cache[key] = ShardedEncoder(original_count, recovery_count, shard_bytes,
-                                                   device=d_recovery.device, group=group, stream=stream,
-                                                   rate_=rate_, ctx=ctx)
+    enc = _sharded(ShardedEncoder, original_count, recovery_count, shard_bytes, d_recovery.device, group, stream,
+                   rate_, ctx)
     _check_matrix(d_recovery, recovery_count, shard_bytes, "d_recovery", on_device=False)
     _check_matrix(d_original, original_count, shard_bytes, "d_original", on_device=False)
     enc(enc.columns(d_original), d_recovery)
+
+
+def decode_device_sharded(original_count: int, recovery_count: int, shard_bytes: int, d_original, original_present,
+                          d_recovery, recovery_present, d_restored, group=None, stream=None,
+                          rate_: int = RATE_DEFAULT, ctx: Optional[Context] = None) -> None:
+    """Multi-GPU decode of one large stripe (ShardedDecoder, cached per shape / group / device):
+    each rank decodes its column slice of d_original [N x S] / d_recovery [M x S] with the
+    erasure pattern evaluated on its own device, and an all-gather writes the missing originals'
+    full rows into d_restored [N x S] on every rank."""
+    dec = _sharded(ShardedDecoder, original_count, recovery_count, shard_bytes, d_restored.device, group, stream,
+                   rate_, ctx)
+    _check_matrix(d_original, original_count, shard_bytes, "d_original", on_device=False)
+    _check_matrix(d_recovery, recovery_count, shard_bytes, "d_recovery", on_device=False)
+    _check_matrix(d_restored, original_count, shard_bytes, "d_restored", on_device=False)
+    dec(dec.columns(d_original), original_present, dec.columns(d_recovery), recovery_present, d_restored)
 
 
 class engine:

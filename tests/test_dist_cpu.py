@@ -157,3 +157,103 @@ def test_bench_gpus_flag_launches_ranks():
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
     assert lines[0]["n_gpus"] == 2 and lines[0]["ranks_seen"] == [0, 1] and lines[0]["steps"] == 3
+
+
+def _worker_sharded_decode(rank, world, port, N, M, S, chunks, q):
+    """ShardedDecoder / decode_device_sharded with the per-piece device decode replaced by the
+    oracle: every rank must end with the missing originals' full rows, present rows untouched."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "reed-solomon-simd_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    import reed_solomon_simd as rs
+    _init(rank, world, port)
+    widths = []
+
+    def piece_standin(orig_cols, op, rec_cols, rp, out):
+        # CPU stand-in for rs_decode_device_strided on a column piece: only missing rows written
+        widths.append(out.shape[1])
+        opa, rpa = np.frombuffer(op, np.uint8), np.frombuffer(rp, np.uint8)
+        got = O.decode("high", np.ascontiguousarray(orig_cols.numpy()), opa, np.ascontiguousarray(rec_cols.numpy()),
+                       rpa)
+        miss = np.flatnonzero(opa == 0)
+        out[torch.from_numpy(miss)] = torch.from_numpy(got[miss])
+
+    try:
+        rng = np.random.default_rng(9)
+        orig = O.generate_original(N, S, 31)
+        rec = O.encode("high", orig, M)
+        L1 = -(-min(N, M) // 100)
+        patterns = [
+            ([1] * (N - L1) + [0] * L1, [1] * L1 + [0] * (M - L1)),              # benchmarks.rs:113-138, 1 %
+            ([1] * (N - min(N, M)) + [0] * min(N, M), [1] * min(N, M) + [0] * (M - min(N, M))),  # 100 %
+        ]
+        lost = rng.choice(N, size=min(N, M) // 3, replace=False)
+        opr = np.ones(N, np.uint8)
+        opr[lost] = 0
+        patterns.append((list(opr), [1] * M))                                 # scattered
+        patterns.append(([1] * N, [0] * M))                                   # nothing to restore
+        dec = rs.ShardedDecoder(N, M, S, rate_=1, decode_slice=piece_standin, chunks=chunks)
+        ok = True
+        for op, rp in patterns:
+            for _ in range(2):  # the second call reuses the pattern's gather buffers
+                out = torch.full((N, S), 0xAB, dtype=torch.uint8)
+                dec(dec.columns(torch.from_numpy(orig)), op, dec.columns(torch.from_numpy(rec)), rp, out)
+                o = out.numpy()
+                miss = np.flatnonzero(np.asarray(op) == 0)
+                keep = np.flatnonzero(np.asarray(op) != 0)
+                ok = ok and bool(np.array_equal(o[miss], orig[miss])) and bool((o[keep] == 0xAB).all())
+        # the cached module-level entry point with the device call replaced
+        rs.decode_device = lambda n, m, w, oc, op, rc, rp, out, stream=None, rate_=0, ctx=None: piece_standin(
+            oc, op, rc, rp, out)
+        out = torch.zeros((N, S), dtype=torch.uint8)
+        op, rp = patterns[0]
+        rs.decode_device_sharded(N, M, S, torch.from_numpy(orig), rs.present_mask(op), torch.from_numpy(rec),
+                                 rs.present_mask(rp), out, rate_=1)
+        miss = np.flatnonzero(np.asarray(op) == 0)
+        ok = ok and bool(np.array_equal(out.numpy()[miss], orig[miss]))
+        q.put((rank, (ok, sorted(set(widths)))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N,M,S,chunks", [(2, 64, 64, 512, 2), (2, 300, 200, 1024, 4), (4, 100, 100, 1024, 4),
+                                                (4, 1000, 1000, 256, 1)])
+def test_column_partitioned_decode(world, N, M, S, chunks):
+    """eval_poly replicated per rank, each rank decodes its column slice, the
+    restored rows are all-gathered and re-interleaved (ShardedDecoder); 1 %, 100 %,
+    scattered and no loss, at world sizes 2 and 4."""
+    out = _spawn(_worker_sharded_decode, world, N, M, S, chunks)
+    # pieces of the explicit decoder, then the whole slice (decode_device_sharded's default for slices < 4 KiB)
+    assert out == {r: (True, sorted({S // world // chunks, S // world})) for r in range(world)}, out
+
+
+def _worker_forced(rank, world, port, q):
+    """world 1 with force_collective: pieces -> all-gather of one rank -> interleave."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "reed-solomon-simd_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    import reed_solomon_simd as rs
+    _init(rank, world, port)
+    try:
+        N, M, S = 200, 100, 512
+        orig = O.generate_original(N, S, 3)
+        want = O.encode("high", orig, M)
+        calls = []
+
+        def enc_standin(cols, out):
+            calls.append(cols.shape[1])
+            out.copy_(torch.from_numpy(O.encode("high", np.ascontiguousarray(cols.numpy()), M)))
+
+        enc = rs.ShardedEncoder(N, M, S, rate_=1, encode_slice=enc_standin, chunks=4, force_collective=True)
+        d_rec = torch.zeros((M, S), dtype=torch.uint8)
+        enc(enc.columns(torch.from_numpy(orig)), d_rec)
+        q.put((rank, (bool(np.array_equal(d_rec.numpy(), want)), enc.collective, calls)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_forced_collective_world1():
+    out = _spawn(_worker_forced, 1)
+    assert out == {0: (True, True, [128] * 4)}

@@ -40,7 +40,7 @@ profile() {  # profile <config-name> <bench args...>
   echo "profiled $cfg"
 }
 
-profile 1024x1024x1k --no-cpu --no-host --no-copy --batch 1 --steps 200 --warmup 20
+profile 1024x1024x1k --no-cpu --no-host --no-copy --no-sharded --batch 1 --steps 200 --warmup 20
 if [ "${CONFIGS:-0}" = "1" ]; then  # the other single-GPU BASELINE configs
   timeout -k 10 300 python -u bench.py --no-cpu --config 32768x32768x1k --steps 50 --warmup 5 \
     > "$OUT/bench_config3.json" 2>> "$OUT/bench.err"

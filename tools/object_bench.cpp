@@ -6,8 +6,13 @@
 // Rust ReedSolomonEncoder / ReedSolomonDecoder takes through the INTEGRATION.md
 // shim, so the rate includes both copies over the host link.
 //
+// Also: a decode with 30 % of the originals lost at random indices (scattered rows),
+// and the one-shot rs_encode / rs_decode (src/lib.rs:251-353), which build a fresh
+// encoder / decoder per call.
+//
 // Usage: rs_object_bench N M S iters warmup  ->  one JSON object on stdout.
 // The restored shards are compared with the originals after the timed calls.
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -86,12 +91,73 @@ int main(int argc, char **argv) {
             ok = ok && p && std::memcmp(p, orig[i].data(), S) == 0;
         }
     }
+    // scattered loss: 30 % of min(N, M) originals at random indices (every lost row its
+    // own run of rows to copy), as many recovery shards from index 0
+    const uint64_t lost_sc = ((N < M ? N : M) * 30 + 99) / 100;
+    std::vector<uint8_t> gone(N, 0);
+    {
+        std::vector<uint64_t> idx(N);
+        for (uint64_t i = 0; i < N; ++i) idx[i] = i;
+        std::shuffle(idx.begin(), idx.end(), gen);
+        for (uint64_t i = 0; i < lost_sc; ++i) gone[idx[i]] = 1;
+    }
+    auto decode_scattered = [&]() {
+        for (uint64_t i = 0; i < N; ++i)
+            if (!gone[i] && (st = rs_decoder_add_original_shard(dec, i, orig[i].data(), S, nullptr)) != RS_OK)
+                die("rs_decoder_add_original_shard", st);
+        for (uint64_t i = 0; i < lost_sc; ++i)
+            if ((st = rs_decoder_add_recovery_shard(dec, i, rec[i].data(), S, nullptr)) != RS_OK)
+                die("rs_decoder_add_recovery_shard", st);
+        if ((st = rs_decoder_decode(dec, nullptr)) != RS_OK) die("rs_decoder_decode", st);
+    };
+    for (int i = 0; i < warmup; ++i) decode_scattered();
+    t0 = now();
+    for (int i = 0; i < iters; ++i) decode_scattered();
+    const double t_sc = (now() - t0) / iters;
+    for (uint64_t i = 0; i < N; ++i)
+        if (gone[i]) {
+            const uint8_t *p = rs_decoder_restored_original(dec, i);
+            ok = ok && p && std::memcmp(p, orig[i].data(), S) == 0;
+        }
+
+    // one-shot rs_encode / rs_decode (lib.rs:251-353): a fresh encoder / decoder per call
+    std::vector<const uint8_t *> optr(N), rptr(M);
+    for (uint64_t i = 0; i < N; ++i) optr[i] = orig[i].data();
+    for (uint64_t i = 0; i < M; ++i) rptr[i] = rec[i].data();
+    std::vector<uint8_t> rec_out(M * S), rest_out(N * S);
+    auto oneshot_enc = [&]() {
+        if ((st = rs_encode(ctx, N, M, S, optr.data(), N, rec_out.data(), nullptr)) != RS_OK) die("rs_encode", st);
+    };
+    for (int i = 0; i < warmup; ++i) oneshot_enc();
+    t0 = now();
+    for (int i = 0; i < iters; ++i) oneshot_enc();
+    const double t_1e = (now() - t0) / iters;
+    for (uint64_t i = 0; i < M; ++i) ok = ok && std::memcmp(&rec_out[i * S], rec[i].data(), S) == 0;
+    const uint64_t lost1 = ((N < M ? N : M) + 99) / 100, have1 = N - lost1;
+    std::vector<uint64_t> oidx(have1), ridx(lost1);
+    for (uint64_t i = 0; i < have1; ++i) oidx[i] = i;
+    for (uint64_t i = 0; i < lost1; ++i) ridx[i] = i;
+    auto oneshot_dec = [&]() {
+        if ((st = rs_decode(ctx, N, M, S, oidx.data(), optr.data(), have1, ridx.data(), rptr.data(), lost1,
+                            rest_out.data(), nullptr, nullptr)) != RS_OK)
+            die("rs_decode", st);
+    };
+    for (int i = 0; i < warmup; ++i) oneshot_dec();
+    t0 = now();
+    for (int i = 0; i < iters; ++i) oneshot_dec();
+    const double t_1d = (now() - t0) / iters;
+    for (uint64_t i = have1; i < N; ++i) ok = ok && std::memcmp(&rest_out[i * S], orig[i].data(), S) == 0;
+
     const double bytes = double(N + M) * double(S), gib = 1024.0 * 1024.0 * 1024.0;
     std::printf(
         "{\"encode_GiBps\": %.3f, \"encode_us\": %.2f, \"decode_1pct_GiBps\": %.3f, \"decode_1pct_us\": %.2f, "
-        "\"decode_100pct_GiBps\": %.3f, \"decode_100pct_us\": %.2f, \"restored_ok\": %s, \"iters\": %d}\n",
+        "\"decode_100pct_GiBps\": %.3f, \"decode_100pct_us\": %.2f, \"decode_scattered30_GiBps\": %.3f, "
+        "\"decode_scattered30_us\": %.2f, \"oneshot_encode_GiBps\": %.3f, \"oneshot_encode_us\": %.2f, "
+        "\"oneshot_decode_1pct_GiBps\": %.3f, \"oneshot_decode_1pct_us\": %.2f, \"restored_ok\": %s, "
+        "\"iters\": %d}\n",
         bytes / t_enc / gib, t_enc * 1e6, bytes / t_dec[0] / gib, t_dec[0] * 1e6, bytes / t_dec[1] / gib,
-        t_dec[1] * 1e6, ok ? "true" : "false", iters);
+        t_dec[1] * 1e6, bytes / t_sc / gib, t_sc * 1e6, bytes / t_1e / gib, t_1e * 1e6, bytes / t_1d / gib,
+        t_1d * 1e6, ok ? "true" : "false", iters);
     rs_decoder_free(dec);
     rs_encoder_free(enc);
     rs_context_destroy(ctx);
