@@ -746,11 +746,11 @@ def test_baseline_decode_8192_64k(torch, rs, loss):
 
 @pytest.mark.parametrize("rate,N,M,S,loss", [("low", 2048, 6144, 65536, 0.5), ("high", 6000, 2000, 65536, 0.3),
                                                ("default", 4096, 4096, 32768, 1.0)])
-def test_streaming_passes_match_oracle(torch, rs, rate, N, M, S, loss):
-    """Matrices of many times the resident workgroups run the streaming pass form
-    (k_pass_stream: each workgroup walks several blocks, loading the next block's rows
-    under the current block's layers): encode on sampled column blocks vs the oracle,
-    decode restores exactly."""
+def test_large_matrix_passes_match_oracle(torch, rs, rate, N, M, S, loss):
+    """Matrices of many times the resident workgroups (more row sets x column slices
+    than the chip holds at once, so each pass's workgroups run in several rounds) on the
+    multi-level pass kernels: encode on sampled column blocks vs the oracle, decode
+    restores exactly."""
     g = torch.Generator(device="cuda")
     g.manual_seed(N + M)
     d_orig = torch.randint(0, 256, (N, S), dtype=torch.uint8, device="cuda", generator=g)
