@@ -326,8 +326,11 @@ rs_status rs_check_device(rs_context *ctx);
  * encodes and decodes of at most half the device's CU count of 4-element packs
  * use packs of 2 elements (twice the workgroups; RS_MI355X_E2_MAX_PACKS sets
  * the limit): adding 8 keeps 4-element packs, adding 16 uses 2-element packs
- * for every single-chunk launch.  A/B and tests; results are identical in
- * every mode. */
+ * for every single-chunk launch.  Single-chunk 2-element encodes of 2^8 and 2^9
+ * rows run on the one-row-per-lane kernel (rs_lane.hip; RS_MI355X_LANE=0 at
+ * context creation: never); adding 32 also runs 2^10-row ones there, adding 64
+ * none.
+ * A/B and tests; results are identical in every mode. */
 rs_status rs_mono_enable(rs_context *ctx, int enable);
 
 /* ---- GF(2^16) tables (src/engine/tables.rs), host copies ---- */

@@ -204,6 +204,13 @@ struct rs_context {
     // with 4-element packs (profiles/r04a/e2_max_packs.txt)
     uint32_t e2_max_packs = 128, e2_default = 128;
     bool e2_encode = true;
+    // one-row-per-lane column kernel (rs_lane.hip) for single-chunk 2-element
+    // encodes of 2^8 .. 2^lane_max_l rows (RS_MI355X_LANE=0/1; rs_mono_enable + 32:
+    // on up to 2^10, + 64: off).  Default 2^9: measured against k_mono (tools/lane_ab.py,
+    // profiles/r05c): 256:256 x 1 KiB 4.72 -> 4.35 us, 512:512 5.61 -> 5.50 us, but
+    // 1024:1024 8.09 -> 8.70 us (its layers' exchange chain is longer than k_mono's)
+    bool lane = true, lane_default = true;
+    int lane_max_l = 9;
     bool pad_small = true;        // decodes of 16..64 work rows on the 2^7-row column kernel (RS_MI355X_PAD_SMALL)
     int chunk_par = -1;           // RS_MI355X_CHUNK_PARALLEL: -1 by pack count (chunk_parallel), 0 / 1 forced
     uint32_t *d_lut2 = nullptr;   // perm2_by_log: the 2-element form of d_lut
@@ -539,6 +546,18 @@ void launch_mono(int mode, uint32_t L, const rs::MonoArgs &M, hipStream_t s, uin
     if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), bytes);
 }
 
+// A single-chunk encode goes to the lane kernel (rs_lane.hip) when enabled and
+// its column arguments are 2-element packs of 2^8..2^10 rows; false: not taken.
+bool try_lane(rs_context *ctx, uint32_t L, uint32_t chunks, const rs::MonoArgs &M, hipStream_t s, uint64_t bytes) {
+    if (!ctx->lane || chunks != 1 || M.elems != 2 || int(L) > ctx->lane_max_l || !rs::lane_supported(int(L)))
+        return false;
+    hipEvent_t ev = nullptr;
+    if (t_prof_ctx) prof_begin(s, &ev);
+    check(rs::launch_lane(int(L), M, s));
+    if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), bytes);
+    return true;
+}
+
 // Single-level multi-chunk encodes: spread the chunks over the grid (grid.y)
 // when the packs alone give few workgroups (RS_MI355X_CHUNK_PARALLEL = 0 / 1
 // forces the serial / parallel form; tools/ab_chunks.sh measures the threshold).
@@ -583,7 +602,8 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
         Mo.ifft_img = 1;  // chunk c: skew offset c * n + n
         Mo.ifft_img_step = 1;
         Mo.fft_img = 0;
-        launch_mono(rs::kMonoEncodeHigh, L, Mo, s, (N + M) * uint64_t(g.packs) * 8 * g.stripes);
+        const uint64_t bytes = (N + M) * uint64_t(g.packs) * 8 * g.stripes;
+        if (!try_lane(ctx, L, C, Mo, s, bytes)) launch_mono(rs::kMonoEncodeHigh, L, Mo, s, bytes);
         return;
     }
     if (lv.m == 1 && (C == 1 || !chunk_parallel(ctx, g, uint64_t(C) * n * g.stride))) {
@@ -666,7 +686,8 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
         Mo.ifft_img = 0;
         Mo.fft_img = 1;  // output chunk c: skew offset c * n + n
         Mo.fft_img_step = 1;
-        launch_mono(rs::kMonoEncodeLow, L, Mo, s, (N + M) * uint64_t(g.packs) * 8 * g.stripes);
+        const uint64_t bytes = (N + M) * uint64_t(g.packs) * 8 * g.stripes;
+        if (!try_lane(ctx, L, C, Mo, s, bytes)) launch_mono(rs::kMonoEncodeLow, L, Mo, s, bytes);
         return;
     }
     if (lv.m == 1) {
@@ -1291,6 +1312,8 @@ rs_status rs_context_create(int device, rs_context **out) {
         int cus = 0;
         check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         ctx->e2_max_packs = ctx->e2_default = cus > 1 ? uint32_t(cus) / 2 : 1u;
+        if (const char *ln = getenv("RS_MI355X_LANE")) ctx->lane = ln[0] == '1';
+        ctx->lane_default = ctx->lane;
         const char *psm = getenv("RS_MI355X_PAD_SMALL");
         if (psm) ctx->pad_small = psm[0] == '1';
         const char *nm = getenv("RS_MI355X_NO_MONO");
@@ -2177,6 +2200,9 @@ rs_status rs_mono_enable(rs_context *ctx, int enable) {
     // + 8: 4-element packs only; + 16: 2-element packs wherever the staged kernel runs
     ctx->e2_max_packs = (enable & 8) ? 0u : (enable & 16) ? 0xFFFFFFFFu : ctx->e2_default;
     ctx->e2_encode = !(enable & 8);
+    // + 32: lane kernel on, + 64: off (neither: the context's default)
+    ctx->lane = (enable & 32) ? true : (enable & 64) ? false : ctx->lane_default;
+    ctx->lane_max_l = (enable & 32) ? 10 : 9;
     return RS_OK;
 }
 

@@ -235,6 +235,12 @@ bool mono_staged(int L, uint32_t chunks);
 bool mono_split(int L);
 int mono_rows_log2_per_lane(int L, uint32_t chunks);
 
+// Lane column kernel (rs_lane.hip): the single-chunk encode of 2^L rows
+// (lane_supported(L): 8 <= L <= 10) in 2-element packs with one row per thread;
+// takes the column kernel's arguments (elems = 2, chunks = 1; stripes for a batch).
+bool lane_supported(int L);
+hipError_t launch_lane(int L, const MonoCore &A, hipStream_t stream);
+
 // eval_poly for a decode (src/engine/utils.rs:20-31) reduced to 2^u points
 // (DESIGN.md "eval_poly"): erasure vector -> per-row log factors.
 //   row r < 2^u: erased bit e(r) (erasure-vector entry) and received bit.

@@ -903,6 +903,58 @@ def test_column_kernel_and_pass_paths_match_oracle(torch, rs, rate, N, M, S, mon
 
 
 # ---------------------------------------------------------------------------
+# one-row-per-lane column kernel (rs_lane.hip): single-chunk 2-element encodes of
+# 2^8 .. 2^10 rows, HighRate and LowRate, tails, strided rows, batches
+
+LANE_CASES = [
+    ("default", 1024, 1024, 1024), ("high", 1000, 1024, 1024), ("high", 700, 513, 512), ("high", 200, 256, 256),
+    ("low", 256, 200, 128), ("low", 400, 500, 64), ("high", 1024, 1024, 130), ("high", 900, 600, 1000),
+    ("low", 129, 256, 6), ("high", 1, 1000, 64), ("high", 512, 512, 2),
+]
+
+
+def _route_of(torch, rs, fn):
+    rs.profile_enable(True)
+    fn()
+    torch.cuda.synchronize()
+    recs = rs.profile_collect()
+    rs.profile_enable(False)
+    return [name for name, _, _ in recs]
+
+
+@pytest.mark.parametrize("rate,N,M,S", LANE_CASES)
+def test_lane_kernel_encode_matches_oracle(torch, rs, rate, N, M, S):
+    rs.mono_enable(1 | 32)
+    try:
+        orig = O.generate_original(N, S, (N + 2 * M + S) & 0xFF)
+        want = O.encode(rate, orig, M)
+        d_o = _dev(torch, orig)
+        d_r = torch.full((M, S), 0xEE, dtype=torch.uint8, device="cuda")
+        route = _route_of(torch, rs, lambda: rs.encode_device(N, M, S, d_o, d_r, rate_=RATE[rate]))
+        assert len(route) == 1 and route[0].startswith("k_lane<"), route
+        assert np.array_equal(d_r.cpu().numpy(), want)
+        # strided rows: column slices of wider matrices (the rows' base and stride differ)
+        wo = torch.full((N, S + 64), 0x11, dtype=torch.uint8, device="cuda")
+        wr = torch.full((M, S + 64), 0x22, dtype=torch.uint8, device="cuda")
+        wo[:, 32:32 + S] = d_o
+        rs.encode_device(N, M, S, wo[:, 32:32 + S], wr[:, 32:32 + S], rate_=RATE[rate])
+        torch.cuda.synchronize()
+        got = wr.cpu().numpy()
+        assert np.array_equal(got[:, 32:32 + S], want)
+        assert np.all(got[:, :32] == 0x22) and np.all(got[:, 32 + S:] == 0x22)
+        # a batch of 3 stripes in one launch
+        origs = [orig] + [O.generate_original(N, S, 90 + b) for b in range(2)]
+        b_o = _dev(torch, np.stack(origs))
+        b_r = torch.empty((3, M, S), dtype=torch.uint8, device="cuda")
+        rs.encode_device_batch(N, M, S, b_o, b_r, rate_=RATE[rate])
+        torch.cuda.synchronize()
+        for b in range(3):
+            assert np.array_equal(b_r[b].cpu().numpy(), O.encode(rate, origs[b], M)), f"stripe {b}"
+    finally:
+        rs.mono_enable(1)
+
+
+# ---------------------------------------------------------------------------
 # host-memory pipeline (column slices over several streams, pinned or pageable buffers)
 
 @pytest.mark.parametrize("rate,N,M,S,slices,pinned", [
