@@ -635,11 +635,27 @@ __device__ __forceinline__ StripeBases stripe_bases(const MonoCore &A, uint32_t 
             const_cast<uint8_t *>(A.dst.base) + uint64_t(stripe) * A.dst_bstride};
 }
 
-__device__ __forceinline__ const uint8_t *row_ptr(const MonoCore &A, const StripeBases &sb, uint32_t r) {
+// Addresses of a lane's rows r0 + D (D a compile-time row offset): one 64-bit
+// multiply per row map for the lane's first row r0, then a uniform step per row
+// (row_ptr per row cost ~30 VALU per row load in the headline encode).  The
+// base addresses may lie outside a map's rows; row_at tests the range first.
+struct RowBase {
+    const uint8_t *p[2];
+    uint32_t r0;
+};
+__device__ __forceinline__ const uint8_t *map_base(const RowMap &m, const uint8_t *base, uint32_t r0) {
+    return base + int64_t(int32_t(r0 - m.row_begin)) * int64_t(m.stride);
+}
+__device__ __forceinline__ RowBase row_base(const MonoCore &A, const StripeBases &sb, uint32_t r0) {
+    return RowBase{{map_base(A.src[0], sb.src0, r0), map_base(A.src[1], sb.src1, r0)}, r0};
+}
+template <uint32_t D>
+__device__ __forceinline__ const uint8_t *row_at(const MonoCore &A, const RowBase &b) {
+    const uint32_t r = b.r0 + D;
     const uint8_t *p = nullptr;
-    if (r >= A.src[0].row_begin && r < A.src[0].row_end) p = sb.src0 + uint64_t(r - A.src[0].row_begin) * A.src[0].stride;
-    if (A.nsrc > 1 && r >= A.src[1].row_begin && r < A.src[1].row_end)
-        p = sb.src1 + uint64_t(r - A.src[1].row_begin) * A.src[1].stride;
+    if (r - A.src[0].row_begin < A.src[0].row_end - A.src[0].row_begin) p = b.p[0] + uint64_t(D) * A.src[0].stride;
+    if (A.nsrc > 1 && r - A.src[1].row_begin < A.src[1].row_end - A.src[1].row_begin)
+        p = b.p[1] + uint64_t(D) * A.src[1].stride;
     return p;
 }
 
@@ -652,6 +668,12 @@ __device__ __forceinline__ const uint8_t *row_ptr(const MonoCore &A, const Strip
 template <typename S, int I, int LR>
 __device__ __forceinline__ uint32_t paired_row(uint32_t lane, uint32_t wave, int j) {
     return lane_rows<S, I>((lane & ~1u) | uint32_t(j & 1), wave) | reg_rows<S, I, LR>(j >> 1);
+}
+// paired_row(lane, wave, j) = paired_row(lane, wave, 0) + paired_delta(j): the lane
+// bit 0 and register bits are clear in the first row
+template <typename S, int I, int LR>
+constexpr uint32_t paired_delta(int j) {
+    return (uint32_t(j & 1) << S::v.maps[I].lane[0]) + reg_rows<S, I, LR>(j >> 1);
 }
 
 // Load transform rows `chunk * n + row` (placement: start of the IFFT) as
@@ -683,10 +705,10 @@ __device__ __forceinline__ void issue_col(const MonoCore &A, uint32_t chunk, con
     const bool bytes = BYTES < 0 ? io.bytes : BYTES != 0;
     PackIO q = io;
     q.bytes = bytes;
+    const RowBase rb = row_base(A, sb, paired_row<S, 0, LR>(lane, wave, 0) + base);
     static_for<0, (2 << LR)>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
-        const uint32_t r = paired_row<S, 0, LR>(lane, wave, j) + base;
-        const uint8_t *p = row_ptr(A, sb, r);
+        const uint8_t *p = row_at<paired_delta<S, 0, LR>(j)>(A, rb);
         const bool ok = p != nullptr && live;
         const uint8_t *a = (ok ? p : any_row) + off;
         uint32_t v;
@@ -696,8 +718,8 @@ __device__ __forceinline__ void issue_col(const MonoCore &A, uint32_t chunk, con
               // zero-extending ushort load gets copied through an AND at the first join)
             v = *reinterpret_cast<const uint32_t *>(a - (reinterpret_cast<uintptr_t>(a) & 3u));
         okm |= uint32_t(ok) << j;
-#ifdef RS_MONO_SKIP_IO
-        v = r * 0x9E3779B9u + off;
+#if defined(RS_MONO_SKIP_IO) || defined(RS_MONO_SKIP_LOADS)
+        v = (rb.r0 + paired_delta<S, 0, LR>(j)) * 0x9E3779B9u + off;
 #endif
         w[j] = v;
     });
@@ -915,17 +937,20 @@ __device__ __forceinline__ void store_col(const MonoCore &A, const uint32_t *row
         xpose<0>(w[2 * i], w[2 * i + 1], lane);
     });
     const uint32_t off = io.lo + ((lane & 1u) ? io.hi_delta : 0u);
+    const uint32_t r0 = paired_row<S, I, LR>(lane, wave, 0) + base;
+    uint8_t *const p0 = const_cast<uint8_t *>(map_base(A.dst, sb.dst, r0));  // (see row_at)
     static_for<0, 2 * R>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
-        const uint32_t r = paired_row<S, I, LR>(lane, wave, j) + base;
-        if (r >= A.dst.row_begin && r < A.dst.row_end) {
+        constexpr uint32_t D = paired_delta<S, I, LR>(j);
+        const uint32_t r = r0 + D;
+        if (r - A.dst.row_begin < A.dst.row_end - A.dst.row_begin) {
             bool keep = true;
             if constexpr (REVEAL) keep = rowinfo[r] & 0x10000u;
-#ifdef RS_MONO_SKIP_IO
+#if defined(RS_MONO_SKIP_IO) || defined(RS_MONO_SKIP_STORES)
             keep = w[j] == 0x12345678u;
 #endif
             if (keep) {
-                uint8_t *p = sb.dst + uint64_t(r - A.dst.row_begin) * A.dst.stride;
+                uint8_t *p = p0 + uint64_t(D) * A.dst.stride;
                 if constexpr (E == 2) st_half(p + off, w[j], io);
 #ifndef RS_MONO_NO_NT_STORE  // streaming (non-temporal) row stores: profiles/r02g/ab_nt
                 else if (!io.bytes) __builtin_nontemporal_store(w[j], reinterpret_cast<uint32_t *>(p + off));
