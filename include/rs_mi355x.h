@@ -329,7 +329,10 @@ rs_status rs_check_device(rs_context *ctx);
  * for every single-chunk launch.  Single-chunk 2-element encodes of 2^8 and 2^9
  * rows run on the one-row-per-lane kernel (rs_lane.hip; RS_MI355X_LANE=0 at
  * context creation: never); adding 32 also runs 2^10-row ones there, adding 64
- * none.
+ * none.  Adding 128 runs single-chunk transforms of 2^12 rows as two launches
+ * of the 2^11-row kernel split by halves of the rows (off by default: slower
+ * than the pass kernels; RS_MI355X_HALF=1 at context creation: on), adding 256
+ * turns that off again.
  * A/B and tests; results are identical in every mode. */
 rs_status rs_mono_enable(rs_context *ctx, int enable);
 

@@ -211,6 +211,14 @@ struct rs_context {
     // 1024:1024 8.09 -> 8.70 us (its layers' exchange chain is longer than k_mono's)
     bool lane = true, lane_default = true;
     int lane_max_l = 9;
+    // half-split 2^12-row transforms (half_split below; RS_MI355X_HALF=0/1;
+    // rs_mono_enable + 128: on, + 256: off).  Off by default: measured slower than
+    // the pass kernels at every shape tried (4096:4096 x 1 KiB encode 19.5 -> 25.0 us,
+    // 2048:2048 x 1 KiB decode 24.8 -> 33.1 us; profiles/r05e/route_half*.jsonl): each
+    // half launch stages a whole 2^11-row twiddle image per workgroup (~3 us of
+    // load issue, profiles/r05e/half_stamps.txt) where a pass stages its sets' tables
+    bool half = false, half_default = false;
+    uint32_t *d_top = nullptr;    // layer-11 perm tables of the half-split kernels (top_table)
     bool pad_small = true;        // decodes of 16..64 work rows on the 2^7-row column kernel (RS_MI355X_PAD_SMALL)
     int chunk_par = -1;           // RS_MI355X_CHUNK_PARALLEL: -1 by pack count (chunk_parallel), 0 / 1 forced
     uint32_t *d_lut2 = nullptr;   // perm2_by_log: the 2-element form of d_lut
@@ -558,6 +566,70 @@ bool try_lane(rs_context *ctx, uint32_t L, uint32_t chunks, const rs::MonoArgs &
     return true;
 }
 
+// Half-split transforms of 2^12 rows (rs_mono.hip kMonoHalf*):
+// the 2^11-row column kernel twice -- kMonoHalfI* runs the IFFT's layers 0..10
+// of each half that holds input rows into the work rows, kMonoHalfF* the top
+// layer (IFFT layer 11, the decode's formal derivative, FFT layer 11) and the
+// FFT's layers 10..0 of each half that holds output rows.  Two launches instead
+// of the pass kernels' three (two for the levels below the top + the fused top)
+// and no separate eval_poly-free row pass; the work rows are written and read
+// once.  Single chunk, one stripe.
+constexpr uint32_t kTopTables = 31;  // skew indices 2047 + 2048 j <= 63487 (65535 entries)
+bool use_half(rs_context *ctx, uint32_t L, const Geom &g, uint32_t chunks) {
+    // (rs_mono_enable 2, MONO_ALL: the unstaged 2^12-row column kernel instead)
+    return ctx->half && ctx->mono && !ctx->mono_all && L == 12 && chunks == 1 && g.stripes == 1 && g.packs <= ctx->mono_max_packs &&
+           rs::mono_staged(11, 1);
+}
+// The top layer's perm table of a transform with skew offset delta (a multiple
+// of 2048): skew index delta + 2047 (engine_naive.rs ifft / fft at dist 2^11).
+const uint32_t *top_table(rs_context *ctx, uint32_t delta, uint32_t elems) {
+    const uint32_t j = delta / 2048;
+    return elems == 2 ? ctx->d_top + kTopTables * rs::kPermWords + j * rs::kPerm2Words : ctx->d_top + j * rs::kPermWords;
+}
+void launch_half(int mode, uint32_t halves, const rs::MonoArgs &M, hipStream_t s, uint64_t bytes) {
+    hipEvent_t ev = nullptr;
+    if (t_prof_ctx) prof_begin(s, &ev);
+    check(rs::launch_mono_half(mode, halves, M, s));
+    if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), bytes);
+}
+// in_halves / out_halves: bit h = half h holds input rows (received rows) /
+// output rows (recovery rows, erased originals); i_delta / f_delta: the IFFT's /
+// FFT's skew offset; rowinfo (decodes): eval_poly's output for the 4096 rows.
+void half_split(rs_context *ctx, Workspace &ws, const Geom &g, bool dec, uint32_t i_delta, uint32_t f_delta,
+                const rs::RowMap *src, uint32_t nsrc, const rs::RowMap &dst, const uint32_t *rowinfo,
+                uint32_t in_halves, uint32_t out_halves, uint64_t in_rows, uint64_t out_rows, hipStream_t s) {
+    if (!in_halves || !out_halves) return;
+    uint8_t *W = static_cast<uint8_t *>(ws.buf[0].get(size_t(4096) * g.stride));
+    Geom g2 = g;
+    g2.stripes = 2;  // the 2-element decision counts both halves' workgroups
+    rs::MonoArgs M = mono_args(ctx, 11, g2, true, dec);
+    M.stripes = 1;
+    M.rowinfo = rowinfo;
+    M.top_i = top_table(ctx, i_delta, M.elems);
+    M.top_f = top_table(ctx, f_delta, M.elems);
+    M.zero_halves = 3u & ~in_halves;
+    const uint64_t row = uint64_t(g.packs) * 8;
+    const uint32_t nin = uint32_t(__builtin_popcount(in_halves)), nout = uint32_t(__builtin_popcount(out_halves));
+    rs::MonoArgs I = M;
+    for (uint32_t k = 0; k < nsrc; ++k) I.src[k] = src[k];
+    I.nsrc = nsrc;
+    I.dst = rs::RowMap{W, g.stride, 0, 4096};
+    I.ifft_img = i_delta / 2048;
+    I.ifft_img_step = 1;
+    I.half0 = in_halves == 2 ? 1 : 0;
+    launch_half(dec ? rs::kMonoHalfIDec : rs::kMonoHalfIEnc, nin, I, s, (in_rows + 2048 * nin) * row);
+    rs::MonoArgs F = M;
+    F.src[0] = rs::RowMap{W, g.stride, 0, 4096};
+    F.nsrc = 1;
+    F.dst = dst;
+    F.fft_img = f_delta / 2048;
+    F.fft_img_step = 1;
+    F.out_half = out_halves == 2 ? 1 : 0;
+    launch_half(dec ? rs::kMonoHalfFDec : rs::kMonoHalfFEnc, nout, F, s, (2048 * nin + out_rows) * row);
+}
+// halves of [b, e) in a 4096-row transform
+uint32_t halves_of(uint64_t b, uint64_t e) { return b >= e ? 0u : (b < 2048 ? 1u : 0u) | (e > 2048 ? 2u : 0u); }
+
 // Single-level multi-chunk encodes: spread the chunks over the grid (grid.y)
 // when the packs alone give few workgroups (RS_MI355X_CHUNK_PARALLEL = 0 / 1
 // forces the serial / parallel form; tools/ab_chunks.sh measures the threshold).
@@ -604,6 +676,10 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
         Mo.fft_img = 0;
         const uint64_t bytes = (N + M) * uint64_t(g.packs) * 8 * g.stripes;
         if (!try_lane(ctx, L, C, Mo, s, bytes)) launch_mono(rs::kMonoEncodeHigh, L, Mo, s, bytes);
+        return;
+    }
+    if (use_half(ctx, L, g, C)) {  // IFFT skew n, FFT skew 0
+        half_split(ctx, ws, g, false, n, 0, &src, 1, dst, nullptr, halves_of(0, N), halves_of(0, M), N, M, s);
         return;
     }
     if (lv.m == 1 && (C == 1 || !chunk_parallel(ctx, g, uint64_t(C) * n * g.stride))) {
@@ -688,6 +764,10 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
         Mo.fft_img_step = 1;
         const uint64_t bytes = (N + M) * uint64_t(g.packs) * 8 * g.stripes;
         if (!try_lane(ctx, L, C, Mo, s, bytes)) launch_mono(rs::kMonoEncodeLow, L, Mo, s, bytes);
+        return;
+    }
+    if (use_half(ctx, L, g, C)) {  // IFFT skew 0, FFT skew n
+        half_split(ctx, ws, g, false, 0, n, &src, 1, dst, nullptr, halves_of(0, N), halves_of(0, M), N, M, s);
         return;
     }
     if (lv.m == 1) {
@@ -948,6 +1028,14 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
     check(rs::launch_eval_poly(E, s));
     if (t_prof_ctx) prof_end(s, ev, "k_eval_poly", uint64_t(nd) * 5);
 
+    if (use_half(ctx, u, g, 1)) {  // IFFT and FFT skew 0 (rate_high.rs:213-245)
+        uint32_t in_h = 0, out_h = 0;
+        for (uint32_t r = 0; r < nd; ++r) in_h |= uint32_t(st[r] == 2) << (r >> 11);
+        for (uint32_t r = out_map.row_begin; r < out_map.row_end; ++r) out_h |= uint32_t(st[r] == 1) << (r >> 11);
+        const rs::RowMap src[2] = {rec_map, orig_map};
+        half_split(ctx, ws, g, true, 0, 0, src, 2, out_map, d_rowinfo, in_h, out_h, received, missing, s);
+        return;
+    }
     rs::PassArgs A = base_args(ctx, g, nd);
     A.rowinfo = d_rowinfo;
     if (mono) {
@@ -1314,6 +1402,19 @@ rs_status rs_context_create(int device, rs_context **out) {
         ctx->e2_max_packs = ctx->e2_default = cus > 1 ? uint32_t(cus) / 2 : 1u;
         if (const char *ln = getenv("RS_MI355X_LANE")) ctx->lane = ln[0] == '1';
         ctx->lane_default = ctx->lane;
+        if (const char *hs = getenv("RS_MI355X_HALF")) ctx->half = hs[0] == '1';
+        ctx->half_default = ctx->half;
+        {  // top_table: skew index 2047 + 2048 j, both table formats
+            std::vector<uint32_t> top(size_t(kTopTables) * (rs::kPermWords + rs::kPerm2Words));
+            for (uint32_t j = 0; j < kTopTables; ++j) {
+                const size_t idx = 2047 + 2048 * size_t(j);
+                std::copy_n(&T.perm_by_skew[idx * rs::kPermWords], rs::kPermWords, &top[j * rs::kPermWords]);
+                std::copy_n(&T.perm2_by_skew[idx * rs::kPerm2Words], rs::kPerm2Words,
+                            &top[kTopTables * rs::kPermWords + j * rs::kPerm2Words]);
+            }
+            check(hipMalloc(&ctx->d_top, top.size() * 4));
+            check(hipMemcpy(ctx->d_top, top.data(), top.size() * 4, hipMemcpyHostToDevice));
+        }
         const char *psm = getenv("RS_MI355X_PAD_SMALL");
         if (psm) ctx->pad_small = psm[0] == '1';
         const char *nm = getenv("RS_MI355X_NO_MONO");
@@ -1354,6 +1455,7 @@ void rs_context_destroy(rs_context *ctx) {
     if (ctx->d_tw) (void)hipFree(ctx->d_tw);
     if (ctx->d_lut) (void)hipFree(ctx->d_lut);
     if (ctx->d_lut2) (void)hipFree(ctx->d_lut2);
+    if (ctx->d_top) (void)hipFree(ctx->d_top);
     for (uint32_t *p : ctx->d_img2)
         if (p) (void)hipFree(p);
     if (ctx->d_lwfold_base) (void)hipFree(ctx->d_lwfold_base);
@@ -2203,6 +2305,8 @@ rs_status rs_mono_enable(rs_context *ctx, int enable) {
     // + 32: lane kernel on, + 64: off (neither: the context's default)
     ctx->lane = (enable & 32) ? true : (enable & 64) ? false : ctx->lane_default;
     ctx->lane_max_l = (enable & 32) ? 10 : 9;
+    // + 128: half-split 2^12-row transforms on, + 256: off
+    ctx->half = (enable & 128) ? true : (enable & 256) ? false : ctx->half_default;
     return RS_OK;
 }
 

@@ -188,7 +188,23 @@ char *launch_name_buf();
 // layer-ordered images: image t (transform skew offset t * n) holds, for
 // layer b = 0..L-1 and group g < n / 2^(b+1), the perm table of skew index
 // g * 2^(b+1) + 2^b + t * n - 1 at table slot n - n / 2^b + g.
-enum MonoMode { kMonoEncodeHigh = 0, kMonoEncodeLow = 1, kMonoDecode = 2 };
+enum MonoMode {
+    kMonoEncodeHigh = 0,
+    kMonoEncodeLow = 1,
+    kMonoDecode = 2,
+    // half-split transforms of 2^12 rows as two launches of 2^11-row column
+    // kernels (L = 11): kMonoHalfI* run the IFFT's layers 0..10 on half
+    // half0 + blockIdx.y of the rows (image ifft_img + half * ifft_img_step) and
+    // store the half's rows to the work rows (dst); kMonoHalfF* load both halves'
+    // work rows, run layer 11 of the IFFT (top_i), the formal derivative (Dec),
+    // layer 11 of the FFT (top_f) and the FFT's layers 10..0 on half
+    // out_half + blockIdx.y (image fft_img + half * fft_img_step), and store /
+    // reveal its rows of dst.  *Dec: the decode's scaling (rowinfo) and reveal.
+    kMonoHalfIEnc = 3,
+    kMonoHalfIDec = 4,
+    kMonoHalfFEnc = 5,
+    kMonoHalfFDec = 6,
+};
 constexpr uint32_t kMonoFusedRows = 2048;  // largest work size of the fused-eval_poly decode
 // The kernel arguments of every column kernel; the staged decode's kernels take
 // MonoArgs (+ the erasure bitmaps), the others this core only: argument bytes
@@ -219,6 +235,10 @@ struct MonoCore {
     // pointers (read only by the batch instantiation)
     uint32_t stripes = 1;
     uint64_t src_bstride[2] = {0, 0}, dst_bstride = 0;
+    // half-split kernels (kMonoHalf*): first half of the launch, halves whose work
+    // rows are all zero (bit h; not read), layer-11 perm tables of the IFFT / FFT
+    uint32_t half0 = 0, zero_halves = 0;
+    const uint32_t *top_i = nullptr, *top_f = nullptr;
 };
 struct MonoArgs : MonoCore {
     // fused-eval_poly decode: erased / received bits of the 2^L work rows, as in EvalArgs
@@ -226,6 +246,8 @@ struct MonoArgs : MonoCore {
 };
 // hipErrorNotSupported: no column kernel for this L (7 <= L <= 12 are built).
 hipError_t launch_mono(int mode, int L, const MonoArgs &A, hipStream_t stream);
+// kMonoHalf* modes: L = 11 only, one stripe, grid.y = halves (launch_mono_half).
+hipError_t launch_mono_half(int mode, uint32_t halves, const MonoArgs &A, hipStream_t stream);
 // Variant launch_mono picks: LDS-staged twiddles (single chunk, 2 rows per
 // lane, L <= 11); fused_eval and stripes > 1 require it.
 bool mono_staged(int L, uint32_t chunks);

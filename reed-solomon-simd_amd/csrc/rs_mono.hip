@@ -42,7 +42,7 @@ __device__ uint64_t g_mono_stamps[4096][24];
 #define RS_MSTAMP(i)                                                                                 \
     do {                                                                                             \
         RS_MSTAMP_WAIT();                                                                            \
-        if (threadIdx.x == blockDim.x - 64 && blockIdx.x < 4096) g_mono_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime(); \
+        if (threadIdx.x == blockDim.x - 64 && blockIdx.x + blockIdx.y * gridDim.x < 4096) g_mono_stamps[blockIdx.x + blockIdx.y * gridDim.x][i] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define RS_MSTAMP(i)
@@ -618,10 +618,10 @@ __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR, E> &c, uint32_t
 // Decode: does this wave hold, after the FFT's remap, any row of A.dst?
 // (there the wave's rows are one block of 2^IW consecutive rows)
 template <int L, int LR, int SPLIT = 0>
-__device__ __forceinline__ bool wave_stores(const MonoCore &A, uint32_t wave) {
+__device__ __forceinline__ bool wave_stores(const MonoCore &A, uint32_t wave, uint32_t base = 0) {
     using S = SeqOf<L, LR, true, SPLIT>;
     constexpr int I = S::v.count;
-    const uint32_t lo = lane_rows<S, I>(0, wave), hi = lo + (1u << (LR + 6));
+    const uint32_t lo = lane_rows<S, I>(0, wave) + base, hi = lo + (1u << (LR + 6));
     return lo < A.dst.row_end && hi > A.dst.row_begin;
 }
 
@@ -683,11 +683,13 @@ constexpr uint32_t paired_delta(int j) {
 // are zeroed by finish_col, not here: a select on the loaded value would make
 // the compiler wait for the load right after issuing it)
 // (2-element packs: the paired words are the 16-bit low and high halves)
-template <int L, int LR, int SPLIT = 0, int E = 4, int BYTES = -1>
+// (AT_FFT: rows in the placement at the start of the FFT -- the end of the IFFT --
+// instead: the half-split kernels' work rows, kMonoHalfF)
+template <int L, int LR, int SPLIT = 0, int E = 4, int BYTES = -1, bool AT_FFT = false>
 __device__ __forceinline__ void issue_col(const MonoCore &A, uint32_t chunk, const PackIO &io, const StripeBases &sb,
                                           uint32_t (&w)[2 << LR], uint32_t &okm, uint32_t lane, uint32_t wave,
                                           bool live = true) {
-    using S = SeqOf<L, LR, false, SPLIT>;
+    using S = SeqOf<L, LR, AT_FFT, SPLIT>;
     const uint32_t base = chunk * (1u << L);
     const uint32_t off = io.lo + ((lane & 1u) ? io.hi_delta : 0u);
     // a row every lane may read (the first source row): lanes without a row of
@@ -878,10 +880,10 @@ __device__ __forceinline__ uint32_t reveal_log(const MonoCore &A, const uint32_t
 }
 template <int L, int LR, int SPLIT = 0>
 __device__ __forceinline__ void reveal_issue(const MonoCore &A, const uint32_t *rowinfo, RevealTabs<LR> &rt,
-                                             uint32_t lane, uint32_t wave) {
+                                             uint32_t lane, uint32_t wave, uint32_t base = 0) {
     using S = SeqOf<L, LR, true, SPLIT>;
     constexpr int I = S::v.count;
-    const uint32_t a = lane_rows<S, I>(lane, wave);
+    const uint32_t a = lane_rows<S, I>(lane, wave) + base;
     static_for<0, (1 << LR)>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         quad_gather2(A.lut, reveal_log<S, I, LR>(A, rowinfo, a | reg_rows<S, I, LR>(i)), lane, rt.t[i]);
@@ -892,11 +894,13 @@ __device__ __forceinline__ void reveal_issue(const MonoCore &A, const uint32_t *
 // of the FFT), paired like the loads.  REVEAL (decode): only erased rows,
 // multiplied by exp(65535 - log factor) (rate_high.rs:241-245); rt: tables
 // from reveal_issue (2-element packs), else gathered here.
-template <int L, int LR, bool REVEAL, int SPLIT = 0, int E = 4>
+// (AT_IFFT: rows in the placement at the end of the IFFT -- the half-split
+// kernels' work rows, kMonoHalfI)
+template <int L, int LR, bool REVEAL, int SPLIT = 0, int E = 4, bool AT_IFFT = false>
 __device__ __forceinline__ void store_col(const MonoCore &A, const uint32_t *rowinfo, uint32_t chunk,
                                           const PackIO &io, const StripeBases &sb, Col<L, LR, E> &c, uint32_t lane,
                                           uint32_t wave, const RevealTabs<LR> *rt = nullptr) {
-    using S = SeqOf<L, LR, true, SPLIT>;
+    using S = SeqOf<L, LR, !AT_IFFT, SPLIT>;
     constexpr uint32_t PC = Fmt<E>::kPC;
     constexpr int I = S::v.count;
     constexpr int R = 1 << LR;
@@ -1442,6 +1446,12 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
         A.src_bstride[1] = K.src_bstride[1];
         A.dst_bstride = K.dst_bstride;
     }
+    if constexpr (MODE >= kMonoHalfIEnc) {  // half-split kernels
+        A.half0 = K.half0;
+        A.zero_halves = K.zero_halves;
+        A.top_i = K.top_i;
+        A.top_f = K.top_f;
+    }
     using C = Col<L, LR, E>;
     // plan kind: split; FLOW for the staged decodes (Plan)
     constexpr int PK = mono_pk(MODE, STAGED, SPLIT);
@@ -1455,8 +1465,11 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
     // XCD-aware: workgroup b runs on XCD b % 8, so the packs of one 64-byte
     // block (which share cache lines) go to one XCD's L2.
 #ifdef RS_MONO_STAMPS  // entry time, before the first kernel-argument load
-    if (threadIdx.x == blockDim.x - 64 && blockIdx.x < 4096) g_mono_stamps[blockIdx.x][7] = __builtin_amdgcn_s_memrealtime();
-    if (threadIdx.x == 0 && blockIdx.x < 4096) g_mono_stamps[blockIdx.x][12] = __builtin_amdgcn_s_memrealtime();
+    {
+        const uint32_t sw = blockIdx.x + blockIdx.y * gridDim.x;
+        if (threadIdx.x == blockDim.x - 64 && sw < 4096) g_mono_stamps[sw][7] = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0 && sw < 4096) g_mono_stamps[sw][12] = __builtin_amdgcn_s_memrealtime();
+    }
 #endif
     const uint32_t b = blockIdx.x;
     const uint32_t pk = (b & 7u) * A.packs_per_xcd + (b >> 3);
@@ -1467,7 +1480,20 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
     const PackIO io = E == 4 ? pack_io(A.fmt, pk) : pack_io2(A.fmt, pk);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t ii = A.ifft_img, fi = A.fft_img;
+    // half-split modes (kMonoHalf*): this workgroup's half; its transform uses one
+    // image for the phase tables (ii = fi: the staged regions serve it alone)
+    constexpr bool HALF_I = MODE == kMonoHalfIEnc || MODE == kMonoHalfIDec;
+    constexpr bool HALF_F = MODE == kMonoHalfFEnc || MODE == kMonoHalfFDec;
+    uint32_t ii = A.ifft_img, fi = A.fft_img, hh = 0;
+    if constexpr (HALF_I) {
+        hh = A.half0 + blockIdx.y;
+        ii += hh * A.ifft_img_step;
+        fi = ii;
+    } else if constexpr (HALF_F) {
+        hh = A.out_half + blockIdx.y;
+        fi += hh * A.fft_img_step;
+        ii = fi;
+    }
     const uint32_t *img_i = A.img + uint64_t(ii) * A.img_words;
     const uint32_t *img_f = A.img + uint64_t(fi) * A.img_words;
     const uint32_t *img_d = A.img + uint64_t(ii ^ fi) * A.img_words;
@@ -1482,6 +1508,9 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             // one chunk in, one chunk out; every table read comes from LDS (layer
             // 0 of phases 1 / 3 from the image when Stage::B0)
             constexpr bool DEC = MODE == kMonoDecode;
+            constexpr bool HSC = MODE == kMonoHalfIDec, HFD = MODE == kMonoHalfFDec;
+            // the half-split kernels' work rows: whole 64-byte blocks
+            const PackIO io_w = E == 4 ? pack_io(ShardFormat{}, pk) : pack_io2(ShardFormat{}, pk);
             uint32_t *shared = lds + G::plane_words;
             // encodes fetch phase 3's tables from the FFT image (requested when phase 1
             // ends); RS_MONO_ENC_DERIVE3: derive them in LDS from phase 1's (+ the D
@@ -1513,11 +1542,11 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             // same tables when IFFT and FFT share the skew offset (decodes,
             // rate_high.rs:213-245), else phase 1's XOR D_b (encodes, Stage::kD)
 #ifndef RS_MONO_NO_REUSE
-            const bool same3 = A.ifft_img == A.fft_img;
+            const bool same3 = ii == fi;
             const bool reuse3 = live && (same3 || kDerive3);
 #else
-            const bool same3 = A.ifft_img == A.fft_img;
-            const bool reuse3 = false;
+            const bool same3 = ii == fi;
+            const bool reuse3 = HALF_F;  // (the half FFT has no IFFT: its region is staged for phase 3)
 #endif
 
             // every global read is requested before any of them is waited for.
@@ -1551,8 +1580,11 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             uint32_t w[2 << LR] = {};
             uint32_t okm = 0;
             auto issue_rows = [&](auto bytes) {
-                issue_col<L, LR, PK, E, decltype(bytes)::value>(A, 0, io, sb, w, okm, lane, wave, live);
+                issue_col<L, LR, PK, E, decltype(bytes)::value>(A, HALF_I ? hh : 0u, io, sb, w, okm, lane, wave, live);
             };
+            // kMonoHalfF: the two halves' IFFT rows (work rows, placement at the FFT's start)
+            uint32_t w2[2 << LR] = {};
+            uint32_t okm2 = 0;
             // phase-1 tables (a live wave loads all of its region's pieces; lanes past
             // the region's end re-read its last piece and do not write it, so the
             // loads are unconditional); B0: layer 0's go into the region first, the
@@ -1615,7 +1647,12 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
 #endif
             };
             using kIO = std::integral_constant<int, kBytesIO>;
-            if constexpr (!DEC) {
+            if constexpr (HALF_F) {
+                issue_col<L, LR, PK, E, 0, true>(A, 0, io_w, sb, w, okm, lane, wave, !(A.zero_halves & 1u));
+                issue_col<L, LR, PK, E, 0, true>(A, 1, io_w, sb, w2, okm2, lane, wave, !(A.zero_halves & 2u));
+                issue_priv();
+                issue_shared();
+            } else if constexpr (!DEC) {
                 issue_rows(kIO{});
                 issue_priv();
                 issue_shared();
@@ -1645,6 +1682,7 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 if constexpr (!kPrivFirst)
                     if (!skip) issue_priv();
             }
+            if constexpr (HSC) scale_issue<L, LR, PK, E>(A, A.rowinfo + (hh << L), st, lane, wave, true);
             RS_MSTAMP(13);
             auto write1 = [&]() {
 #ifndef RS_MONO_SKIP_STAGE
@@ -1656,7 +1694,7 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             };
 #ifndef RS_MONO_SKIP_STAGE
             if (!skip) {  // (a skipping wave's region is written by phase 3's tables before use)
-                if constexpr (G::B0)
+                if constexpr (G::B0 && !HALF_F)
                     static_for<0, KP0>([&](auto kc) {
                         const uint32_t q = lane + 64u * decltype(kc)::value;
                         if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at0(q)] = v0[kc];
@@ -1669,7 +1707,13 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 if (q < PC * kSh) reinterpret_cast<uint4 *>(shared)[G::atS(q)] = vs[kc];
             });
 #endif
-            finish_col<L, LR, DEC>(w, okm, &st, c, lane, io);
+            C cb;  // kMonoHalfF: the upper half's rows
+            if constexpr (HALF_F) {
+                finish_col<L, LR, false>(w, okm, &st, c, lane, io_w);
+                finish_col<L, LR, false>(w2, okm2, &st, cb, lane, io_w);
+            } else {
+                finish_col<L, LR, DEC || HSC>(w, okm, &st, c, lane, io);
+            }
             RS_MSTAMP(1);
             const LdsTabs<L, LR, PK, E> ts{priv, shared, img_i, img_f};
             // phase-3 tables: requested when phase 1 ends, written over this wave's
@@ -1730,14 +1774,14 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             };
             // 2-element decodes: the reveal tables are requested just before the FFT's
             // last remap (with phase 3's table writes), so they land while phase 3 runs
-            constexpr bool kPreReveal = DEC && E == 2 && kQuadGather;
+            constexpr bool kPreReveal = (DEC || HFD) && E == 2 && kQuadGather;
             RevealTabs<LR> rt;
             auto pre3 = [&](bool alive) {
                 return [&, alive]() {
                     write3();
                     (void)alive;
                     if constexpr (kPreReveal)
-                        if (alive) reveal_issue<L, LR, PK>(A, ri, rt, lane, wave);
+                        if (alive) reveal_issue<L, LR, PK>(A, ri, rt, lane, wave, HFD ? hh << L : 0u);
                 };
             };
             if constexpr (SPLIT) {
@@ -1764,9 +1808,58 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, PK>(ts, c, plane, lane, wave, pre3(alive),
                                                                                   alive, out, write4);
                 if (!alive) return;
+            } else if constexpr (HALF_F) {
+                static_assert(G::WB > 0, "half FFT: the 2^11-row plan");
+                // rate_high.rs:235-237 across the halves (a: lower, b: upper row of a pair):
+                // IFFT layer 11 (engine_naive.rs:96-100), the formal derivative (closed
+                // form: each half's own terms, plus the upper partner for lower rows;
+                // utils.rs:99-104), FFT layer 11 (engine_naive.rs:64-68)
+                constexpr int TW = Fmt<E>::kTW;
+                uint32_t ti[TW], tf[TW];
+                static_for<0, TW / 4>([&](auto qc) {
+                    constexpr int q = decltype(qc)::value;
+                    const uint4 x = reinterpret_cast<const uint4 *>(A.top_i)[q];
+                    const uint4 y = reinterpret_cast<const uint4 *>(A.top_f)[q];
+                    ti[4 * q] = x.x, ti[4 * q + 1] = x.y, ti[4 * q + 2] = x.z, ti[4 * q + 3] = x.w;
+                    tf[4 * q] = y.x, tf[4 * q + 1] = y.y, tf[4 * q + 2] = y.z, tf[4 * q + 3] = y.w;
+                });
+                static_for<0, R>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    if constexpr (E == 2) ifft_bfly2(c.lo[i], cb.lo[i], ti);
+                    else ifft_bfly(c.lo[i], c.hi[i], cb.lo[i], cb.hi[i], ti);
+                });
+                if constexpr (HFD) {
+                    const C bp = cb;
+                    formal_derivative<L, LR>(c, plane, lane, wave);
+                    formal_derivative<L, LR>(cb, plane, lane, wave);
+                    static_for<0, R>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value;
+                        c.lo[i] ^= bp.lo[i];
+                        if constexpr (E == 4) c.hi[i] ^= bp.hi[i];
+                    });
+                }
+                static_for<0, R>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    if constexpr (E == 2) fft_bfly2(c.lo[i], cb.lo[i], tf);
+                    else fft_bfly(c.lo[i], c.hi[i], cb.lo[i], cb.hi[i], tf);
+                });
+                if (hh & 1u) c = cb;
+                RS_MSTAMP(6);
+                using SF = SeqOf<L, LR, true, PK>;
+                constexpr int NLF = num_layers(SF::v);
+                const bool alive = !HFD || wave_stores<L, LR, PK>(A, wave, hh << L);
+                issue4(alive);
+                run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, PK>(ts, c, plane, lane, wave, pre3(alive),
+                                                                                alive, true, write4);
+                if (!alive) return;
             } else if constexpr (G::WB > 0) {
                 run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 1 : -1, PK>(ts, c, plane, lane, wave, issue3, true, live,
                                                                        write1);
+                if constexpr (HALF_I) {  // the half's IFFT rows to the work rows; no FFT here
+                    store_col<L, LR, false, PK, E, true>(A, ri, hh, io_w, sb, c, lane, wave);
+                    RS_MSTAMP(11);
+                    return;
+                }
                 RS_MSTAMP(5);
                 using SF = SeqOf<L, LR, true, PK>;
                 constexpr int NLF = num_layers(SF::v);
@@ -1785,7 +1878,8 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 run_seq<L, LR, true, RS_MONO_LDS_PF, -1, PK>(ts, c, plane, lane, wave, NoHook{});
             }
             RS_MSTAMP(10);
-            store_col<L, LR, DEC, PK>(A, ri, 0, io, sb, c, lane, wave, kPreReveal && G::WB > 0 ? &rt : nullptr);
+            store_col<L, LR, DEC || HFD, PK>(A, ri, HALF_F ? hh : 0u, io, sb, c, lane, wave,
+                                             kPreReveal && G::WB > 0 ? &rt : nullptr);
             RS_MSTAMP(11);
       };
       if constexpr (MODE == kMonoDecode) {
@@ -1930,6 +2024,43 @@ hipError_t launch_m(int L, const MonoArgs &A, hipStream_t s) {
 }
 
 }  // namespace
+
+hipError_t launch_mono_half(int mode, uint32_t halves, const MonoArgs &A, hipStream_t s) {
+    if (A.packs == 0 || halves == 0) return hipSuccess;
+    if (halves > 2 || A.stripes != 1 || A.chunks != 1) return hipErrorInvalidValue;
+    if constexpr (!RS_MONO_HAS_L(11)) {
+        return hipErrorNotSupported;
+    } else {
+        auto go = [&](auto mc, auto ec) -> hipError_t {
+            constexpr int MODE = decltype(mc)::value, E = decltype(ec)::value;
+            constexpr int L = 11, LR = mono_lr(L, true);
+            using G = Stage<L, LR, mono_pk(MODE, true, false), E>;
+            size_t lds = size_t(G::words_enc) * 4;
+            if (E == 2 && lds <= 80 * 1024) lds = 84 * 1024;
+            static std::atomic<uint64_t> attr_devs{0};
+            hipError_t e = lds_attr_once(attr_devs, reinterpret_cast<const void *>(&k_mono<L, LR, MODE, true, false, false, E>),
+                                         int(lds));
+            if (e != hipSuccess) return e;
+            k_mono<L, LR, MODE, true, false, false, E>
+                <<<dim3(8u * A.packs_per_xcd, halves), 1 << (L - LR), lds, s>>>(static_cast<const MonoCore &>(A));
+            snprintf(launch_name_buf(), kLaunchNameBytes, "k_mono<%d, %d, %d, true, false, false, %d>", L, LR, MODE, E);
+            return hipGetLastError();
+        };
+        using I2 = std::integral_constant<int, 2>;
+        using I4 = std::integral_constant<int, 4>;
+        switch (mode) {
+            case kMonoHalfIEnc: return A.elems == 2 ? go(std::integral_constant<int, kMonoHalfIEnc>{}, I2{})
+                                                    : go(std::integral_constant<int, kMonoHalfIEnc>{}, I4{});
+            case kMonoHalfIDec: return A.elems == 2 ? go(std::integral_constant<int, kMonoHalfIDec>{}, I2{})
+                                                    : go(std::integral_constant<int, kMonoHalfIDec>{}, I4{});
+            case kMonoHalfFEnc: return A.elems == 2 ? go(std::integral_constant<int, kMonoHalfFEnc>{}, I2{})
+                                                    : go(std::integral_constant<int, kMonoHalfFEnc>{}, I4{});
+            case kMonoHalfFDec: return A.elems == 2 ? go(std::integral_constant<int, kMonoHalfFDec>{}, I2{})
+                                                    : go(std::integral_constant<int, kMonoHalfFDec>{}, I4{});
+            default: return hipErrorNotSupported;
+        }
+    }
+}
 
 bool mono_staged(int L, uint32_t chunks) { return L >= 7 && staged_l(L) && chunks == 1; }
 bool mono_split(int L) { return split_l(L) && staged_l(L); }

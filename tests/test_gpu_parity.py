@@ -955,6 +955,108 @@ def test_lane_kernel_encode_matches_oracle(torch, rs, rate, N, M, S):
 
 
 # ---------------------------------------------------------------------------
+# half-split 2^12-row transforms (rs_codec.cpp half_split, rs_mono_enable + 128; off by
+# default, slower than the passes): two launches of the 2^11-row column kernel -- the IFFT
+# below the top layer per half with input rows, then the top layer (+ the decode's formal
+# derivative) and the FFT per half with output rows
+
+HALF_ENC = [
+    # (rate, N, M, S): single-chunk encodes of 2^12 rows; inputs / outputs in one or both halves
+    ("high", 4096, 4096, 1024), ("high", 2000, 3000, 256), ("high", 4000, 2500, 130), ("high", 1, 2049, 64),
+    ("low", 4096, 4096, 64), ("low", 3000, 1000, 64), ("low", 2500, 4000, 6), ("low", 4096, 1, 2),
+]
+HALF_DEC = [
+    # (rate, N, M, S, pattern): 4096 work rows; "lost_all": every original lost, so the
+    # received rows lie in one half (the other half's IFFT is not launched)
+    ("high", 2048, 2048, 1024, "random"), ("high", 2048, 2048, 64, "lost_all"), ("high", 3000, 1000, 128, "random"),
+    ("low", 2000, 2000, 64, "random"), ("low", 1024, 3000, 130, "random"), ("low", 2000, 2000, 6, "lost_all"),
+    ("high", 2048, 2048, 1024, "one"),
+]
+
+
+def _half_modes(route, dec):
+    """kMonoHalf* modes (rs_device.hpp MonoMode) in launch order"""
+    return [int(n.split(",")[2]) for n in route if n.startswith("k_mono<11,")]
+
+
+@pytest.mark.parametrize("mono", [1 | 128, 1 | 8 | 128, 1 | 16 | 128])
+@pytest.mark.parametrize("rate,N,M,S", HALF_ENC)
+def test_half_split_encode_matches_oracle(torch, rs, rate, N, M, S, mono):
+    rs.mono_enable(mono)
+    try:
+        orig = O.generate_original(N, S, (N + 5 * M + S) & 0xFF)
+        want = O.encode(rate, orig, M)
+        d_o = _dev(torch, orig)
+        d_r = torch.full((M, S), 0xEE, dtype=torch.uint8, device="cuda")
+        route = _route_of(torch, rs, lambda: rs.encode_device(N, M, S, d_o, d_r, rate_=RATE[rate]))
+        assert _half_modes(route, False) == [3, 5] and len(route) == 2, route
+        assert np.array_equal(d_r.cpu().numpy(), want)
+        # strided rows: column slices of wider matrices
+        wo = torch.full((N, S + 64), 0x11, dtype=torch.uint8, device="cuda")
+        wr = torch.full((M, S + 64), 0x22, dtype=torch.uint8, device="cuda")
+        wo[:, 32:32 + S] = d_o
+        rs.encode_device(N, M, S, wo[:, 32:32 + S], wr[:, 32:32 + S], rate_=RATE[rate])
+        torch.cuda.synchronize()
+        got = wr.cpu().numpy()
+        assert np.array_equal(got[:, 32:32 + S], want)
+        assert np.all(got[:, :32] == 0x22) and np.all(got[:, 32 + S:] == 0x22)
+    finally:
+        rs.mono_enable(1)
+
+
+@pytest.mark.parametrize("mono", [1 | 128, 1 | 8 | 128, 1 | 16 | 128])
+@pytest.mark.parametrize("rate,N,M,S,kind", HALF_DEC)
+def test_half_split_decode_matches_oracle(torch, rs, rate, N, M, S, kind, mono):
+    rs.mono_enable(mono)
+    try:
+        rng = np.random.default_rng(N + 7 * M + S)
+        orig = O.generate_original(N, S, (N + M + S) & 0xFF)
+        rec = O.encode(rate, orig, M)
+        op = np.ones(N, np.uint8)
+        if kind == "lost_all":
+            op[:] = 0
+        elif kind == "one":
+            op[N // 3] = 0
+        else:
+            op[rng.choice(N, max(1, min(N, M) // 3), replace=False)] = 0
+        lost = int((op == 0).sum())
+        rp = np.zeros(M, np.uint8)
+        rp[rng.choice(M, lost, replace=False)] = 1
+        want = O.decode(rate, orig, op, rec, rp)
+        d_o = _dev(torch, np.where(op[:, None] == 1, orig, 0xA5).astype(np.uint8))
+        d_r = _dev(torch, np.where(rp[:, None] == 1, rec, 0x5A).astype(np.uint8))
+        d_out = torch.full((N, S), 0x33, dtype=torch.uint8, device="cuda")
+        route = _route_of(torch, rs, lambda: rs.decode_device(N, M, S, d_o, op, d_r, rp, d_out, rate_=RATE[rate]))
+        assert _half_modes(route, True) == [4, 6] and len(route) == 3, route  # + k_eval_poly
+        got = d_out.cpu().numpy()
+        miss = op == 0
+        assert np.array_equal(got[miss], orig[miss]) and np.array_equal(got[miss], want[miss])
+        assert np.all(got[~miss] == 0x33), "present rows of the output must not be written"
+        rs.check_device()
+    finally:
+        rs.mono_enable(1)
+
+
+def test_half_split_off_matches_on(torch, rs):
+    """rs_mono_enable + 256 (half-split off: the pass kernels) and + 128 give the same bytes."""
+    N, M, S = 4096, 4096, 512
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    d_o = torch.randint(0, 256, (N, S), dtype=torch.uint8, device="cuda", generator=g)
+    outs = []
+    for mode in (1 | 256, 1 | 128):
+        rs.mono_enable(mode)
+        try:
+            d_r = torch.empty((M, S), dtype=torch.uint8, device="cuda")
+            rs.encode_device(N, M, S, d_o, d_r)
+            torch.cuda.synchronize()
+            outs.append(d_r)
+        finally:
+            rs.mono_enable(1)
+    assert torch.equal(outs[0], outs[1])
+
+
+# ---------------------------------------------------------------------------
 # host-memory pipeline (column slices over several streams, pinned or pageable buffers)
 
 @pytest.mark.parametrize("rate,N,M,S,slices,pinned", [

@@ -236,3 +236,38 @@ def test_random_work_reuse(rs, seq):
         got = dict(dec.decode().restored_original_iter())
         assert sorted(got) == [int(i) for i in np.flatnonzero(op == 0)]
         assert all(got[i] == orig[i].tobytes() for i in got), "decode"
+
+
+def _half_cases(count):
+    """2^12-row single-chunk encodes and 4096-work-row decodes for the half-split route
+    (rs_codec.cpp half_split, on with rs_mono_enable + 128)."""
+    rng = np.random.default_rng(SEED + 2)
+    out = []
+    while len(out) < count:
+        rate = ["high", "low"][int(rng.integers(0, 2))]
+        big = int(rng.integers(2049, 4097))
+        if rng.random() < 0.5:  # encode transform of 2^12 rows (one chunk)
+            small = int(rng.integers(1, 4097))
+            N, M = (small, big) if rate == "high" else (big, small)
+        else:  # decode work rows pow2(chunk) + other in (2048, 4096]
+            chunk_n = int(rng.integers(1, 2049))
+            other = int(rng.integers(max(1, 2049 - P2(chunk_n)), 4096 - P2(chunk_n) + 1))
+            N, M = (other, chunk_n) if rate == "high" else (chunk_n, other)
+        if not _supported(N, M, rate):
+            continue
+        S = _even(rng, 2, 256)
+        if rng.random() < 0.3 and S % 64 == 0:
+            S += 2
+        op, rp, how = _losses(rng, N, M, rate)
+        seed = int(rng.integers(0, 256))
+        out.append(pytest.param(rate, N, M, S, op, rp, seed, id=f"half{len(out)}-{rate}-{N}x{M}x{S}-{how}"))
+    return out
+
+
+@pytest.mark.parametrize("rate,N,M,S,op,rp,seed", _half_cases(40))
+def test_random_half_split_route(torch, rs, rate, N, M, S, op, rp, seed):
+    rs.mono_enable(1 | 128)
+    try:
+        test_random_encode_decode_device(torch, rs, rate, N, M, S, op, rp, seed)
+    finally:
+        rs.mono_enable(1)

@@ -104,8 +104,41 @@ int main(int argc, char **argv) {
             else A.erased[r >> 5] |= 1u << (r & 31);
         }
     }
+    // "hi" / "hf" (n = 2048): the half-split kernels of a 4096:4096 HighRate encode,
+    // kMonoHalfIEnc (IFFT halves into the work rows) / kMonoHalfFEnc (top layer + FFT halves)
+    uint32_t halves = 0;
+    if (argc > 3 && argv[3][0] == 'h') {
+        uint8_t *o2, *w2, *r2;
+        CK(hipMalloc(&o2, size_t(2 * n) * S));
+        CK(hipMalloc(&w2, size_t(2 * n) * S));
+        CK(hipMalloc(&r2, size_t(2 * n) * S));
+        CK(hipMemset(o2, 0x37, size_t(2 * n) * S));
+        CK(hipMemset(w2, 0x21, size_t(2 * n) * S));
+        std::vector<uint32_t> top(2 * tw);
+        for (int k = 0; k < 2; ++k)  // skew index 2047 + delta: delta 4096 (IFFT), 0 (FFT)
+            std::copy_n(&skew_tabs[size_t(2047 + (k == 0 ? 4096 : 0)) * tw], tw, &top[k * tw]);
+        uint32_t *d_top;
+        CK(hipMalloc(&d_top, top.size() * 4));
+        CK(hipMemcpy(d_top, top.data(), top.size() * 4, hipMemcpyHostToDevice));
+        A.top_i = d_top;
+        A.top_f = d_top + tw;
+        halves = 2;
+        if (argv[3][1] == 'i') {
+            mode = rs::kMonoHalfIEnc;
+            A.src[0] = rs::RowMap{o2, S, 0, 2 * n};
+            A.dst = rs::RowMap{w2, S, 0, 2 * n};
+            A.ifft_img = 2;
+            A.ifft_img_step = 1;
+        } else {
+            mode = rs::kMonoHalfFEnc;
+            A.src[0] = rs::RowMap{w2, S, 0, 2 * n};
+            A.dst = rs::RowMap{r2, S, 0, 2 * n};
+            A.fft_img = 0;
+            A.fft_img_step = 1;
+        }
+    }
     const int iters = 1000;
-    auto go = [&] { CK(rs::launch_mono(mode, int(L), A, 0)); };
+    auto go = [&] { CK(halves ? rs::launch_mono_half(mode, halves, A, 0) : rs::launch_mono(mode, int(L), A, 0)); };
     for (int i = 0; i < 20; ++i) go();
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
@@ -135,7 +168,7 @@ int main(int argc, char **argv) {
     CK(hipDeviceSynchronize());
     go();
     CK(hipDeviceSynchronize());
-    const uint32_t wgs = 8 * A.packs_per_xcd;
+    const uint32_t wgs = 8 * A.packs_per_xcd * (halves ? halves : 1);
     std::vector<uint64_t> st(4096 * 24);
     CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(rs::g_mono_stamps), st.size() * 8));
     // s_memrealtime is per XCD: entry spread within each XCD's workgroups
