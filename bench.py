@@ -155,8 +155,15 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
+    if os.environ.get("RS_BENCH_REHEARSE") == "1":
+        # rehearsal of the N-rank path on a one-GPU box: every rank on cuda:0, collectives on
+        # gloo (numbers meaningless; the driver's N-GPU runs use RCCL, one GPU per rank)
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("RS_BENCH_REHEARSE") == "1":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         world = dist.get_world_size()
     torch.cuda.set_device(local)
     import reed_solomon_simd as rs
@@ -546,7 +553,11 @@ def sharded_block(args, rs, ctx, world, rank, dev):
            "allgather_and_interleave_ms": round((t_step - t_comp) * 1e3, 4),
            "pipeline_pieces": enc.chunks if world > 1 else 1,
            "per_gpu_roofline": {k: rl[k] for k in ("kernel", "achieved", "frac", "traffic", "valu_frac")},
-           "parallelism": f"column partition x{world}" + (" + all_gather_into_tensor (RCCL)" if world > 1 else "")}
+           "parallelism": f"column partition x{world}" + (
+               "" if world == 1 else " + all_gather (gloo rehearsal on one GPU)"
+               if os.environ.get("RS_BENCH_REHEARSE") == "1" else " + all_gather_into_tensor (RCCL)")}
+    if world > 1:  # the committed PMC figures are the whole matrix's (N = 1), not a slice's
+        out["per_gpu_roofline"].update(traffic=None, valu_frac=None)
     del enc
     # column-partitioned decode at 1 % loss: every rank restores the lost originals' full rows
     L = -(-min(N, M) // 100)
