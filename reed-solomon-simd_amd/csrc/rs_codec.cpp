@@ -218,6 +218,10 @@ struct rs_context {
     // half launch stages a whole 2^11-row twiddle image per workgroup (~3 us of
     // load issue, profiles/r05e/half_stamps.txt) where a pass stages its sets' tables
     bool half = false, half_default = false;
+    // multi-chunk encodes of 2^2..2^7-row transforms on k_chunks (use_chunks below;
+    // RS_MI355X_CHUNKS=0/1; rs_mono_enable + 512: on, + 1024: off)
+    bool chunks = true, chunks_default = true;
+    bool chunks_forced = false;  // every multi-chunk shape k_chunks supports (+ 512)
     uint32_t *d_top = nullptr;    // layer-11 perm tables of the half-split kernels (top_table)
     bool pad_small = true;        // decodes of 16..64 work rows on the 2^7-row column kernel (RS_MI355X_PAD_SMALL)
     int chunk_par = -1;           // RS_MI355X_CHUNK_PARALLEL: -1 by pack count (chunk_parallel), 0 / 1 forced
@@ -488,6 +492,8 @@ void run_level(rs::PassArgs A, const Levels &lv, uint32_t k, int flags, uint32_t
 // every skew offset t * n, t = 0 .. 65536/n - 1 (rs_device.hpp), built on the
 // host from the skew tables once per context and L.
 constexpr uint32_t kMonoMinL = 7, kMonoMaxL = 12;
+constexpr uint32_t kChunksMinL = 2;  // k_chunks' smallest transform (images built from here)
+constexpr uint32_t kChunksMaxWaves = 8;  // k_chunks' waves per workgroup (rs_chunks.hip kMaxWaves)
 const uint32_t *mono_images(rs_context *ctx, uint32_t L, uint32_t elems = 4) {
     std::lock_guard<std::mutex> lock(ctx->img_mu);
     uint32_t *&slot_ptr = elems == 2 ? ctx->d_img2[L] : ctx->d_img[L];
@@ -564,6 +570,37 @@ bool try_lane(rs_context *ctx, uint32_t L, uint32_t chunks, const rs::MonoArgs &
     check(rs::launch_lane(int(L), M, s));
     if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), bytes);
     return true;
+}
+
+// Multi-chunk encodes of small transforms (rs_chunks.hip): one launch in which the
+// waves of a pack's workgroup take the chunks in parallel (HighRate input chunks,
+// LowRate output chunks).  One stripe; the column kernel's pack bound.  Routed
+// by default where it measured faster than the passes (profiles/r05g): HighRate
+// with at most one chunk per wave (1000:100 x 1 KiB 13.2 -> 10.9 us, 500:64 10.3 ->
+// 7.8, 100:10 18.5 -> 8.6); LowRate (one pass, the output chunks over the grid) and
+// more chunks than waves stay on the passes unless forced (rs_mono_enable + 512).
+bool use_chunks(rs_context *ctx, uint32_t L, const Geom &g, uint32_t chunks, bool high) {
+    // (RS_MI355X_CHUNK_PARALLEL forces one of the pass forms: tests, A/B)
+    if (!ctx->chunks || !ctx->mono || ctx->mono_all || ctx->chunk_par >= 0 || chunks < 2 || g.stripes != 1 ||
+        !rs::chunks_supported(int(L)) || g.packs > ctx->mono_max_packs)
+        return false;
+    return ctx->chunks_forced || (high && chunks <= kChunksMaxWaves);
+}
+void launch_chunks(rs_context *ctx, const Geom &g, bool high, uint32_t L, const rs::RowMap &src, const rs::RowMap &dst,
+                   uint32_t chunks, uint64_t bytes, hipStream_t s) {
+    rs::MonoArgs Mo = mono_args(ctx, L, g, true);
+    Mo.src[0] = src;
+    Mo.nsrc = 1;
+    Mo.dst = dst;
+    Mo.chunks = chunks;
+    Mo.ifft_img = high ? 1 : 0;  // HighRate chunk c: skew offset c n + n; LowRate: 0
+    Mo.ifft_img_step = high ? 1 : 0;
+    Mo.fft_img = high ? 0 : 1;  // LowRate output chunk c: skew offset c n + n
+    Mo.fft_img_step = high ? 0 : 1;
+    hipEvent_t ev = nullptr;
+    if (t_prof_ctx) prof_begin(s, &ev);
+    check(rs::launch_chunks(int(L), high, Mo, s));
+    if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), bytes);
 }
 
 // Half-split transforms of 2^12 rows (rs_mono.hip kMonoHalf*):
@@ -678,6 +715,10 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
         if (!try_lane(ctx, L, C, Mo, s, bytes)) launch_mono(rs::kMonoEncodeHigh, L, Mo, s, bytes);
         return;
     }
+    if (use_chunks(ctx, L, g, C, true)) {
+        launch_chunks(ctx, g, true, L, src, dst, C, (N + M) * uint64_t(g.packs) * 8, s);
+        return;
+    }
     if (use_half(ctx, L, g, C)) {  // IFFT skew n, FFT skew 0
         half_split(ctx, ws, g, false, n, 0, &src, 1, dst, nullptr, halves_of(0, N), halves_of(0, M), N, M, s);
         return;
@@ -764,6 +805,10 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
         Mo.fft_img_step = 1;
         const uint64_t bytes = (N + M) * uint64_t(g.packs) * 8 * g.stripes;
         if (!try_lane(ctx, L, C, Mo, s, bytes)) launch_mono(rs::kMonoEncodeLow, L, Mo, s, bytes);
+        return;
+    }
+    if (use_chunks(ctx, L, g, C, false)) {
+        launch_chunks(ctx, g, false, L, src, dst, C, (N + M) * uint64_t(g.packs) * 8, s);
         return;
     }
     if (use_half(ctx, L, g, C)) {  // IFFT skew 0, FFT skew n
@@ -1404,6 +1449,8 @@ rs_status rs_context_create(int device, rs_context **out) {
         ctx->lane_default = ctx->lane;
         if (const char *hs = getenv("RS_MI355X_HALF")) ctx->half = hs[0] == '1';
         ctx->half_default = ctx->half;
+        if (const char *ck = getenv("RS_MI355X_CHUNKS")) ctx->chunks = ck[0] == '1';
+        ctx->chunks_default = ctx->chunks;
         {  // top_table: skew index 2047 + 2048 j, both table formats
             std::vector<uint32_t> top(size_t(kTopTables) * (rs::kPermWords + rs::kPerm2Words));
             for (uint32_t j = 0; j < kTopTables; ++j) {
@@ -1435,8 +1482,8 @@ rs_status rs_context_create(int device, rs_context **out) {
         // column-kernel twiddle images of every transform size, built now: a lazy
         // build inside an asynchronous call would stall the device with a
         // synchronous upload the first time a size is seen
-        for (uint32_t L = kMonoMinL; L <= kMonoMaxL; ++L) mono_images(ctx, L);
-        for (uint32_t L = kMonoMinL; L <= 11; ++L) mono_images(ctx, L, 2);
+        for (uint32_t L = kChunksMinL; L <= kMonoMaxL; ++L) mono_images(ctx, L);
+        for (uint32_t L = kChunksMinL; L <= 11; ++L) mono_images(ctx, L, 2);
         return RS_OK;
     });
     if (st != RS_OK) {
@@ -2307,6 +2354,9 @@ rs_status rs_mono_enable(rs_context *ctx, int enable) {
     ctx->lane_max_l = (enable & 32) ? 10 : 9;
     // + 128: half-split 2^12-row transforms on, + 256: off
     ctx->half = (enable & 128) ? true : (enable & 256) ? false : ctx->half_default;
+    // + 512: multi-chunk kernel on, + 1024: off
+    ctx->chunks = (enable & 512) ? true : (enable & 1024) ? false : ctx->chunks_default;
+    ctx->chunks_forced = (enable & 512) != 0;
     return RS_OK;
 }
 

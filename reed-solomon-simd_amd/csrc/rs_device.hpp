@@ -246,6 +246,14 @@ struct MonoArgs : MonoCore {
 };
 // hipErrorNotSupported: no column kernel for this L (7 <= L <= 12 are built).
 hipError_t launch_mono(int mode, int L, const MonoArgs &A, hipStream_t stream);
+// Multi-chunk encodes of 2^L rows, 2 <= L <= 7 (rs_chunks.hip): HighRate (high:
+// A.chunks input chunks, images ifft_img + c * ifft_img_step, fft_img) or
+// LowRate (A.chunks output chunks, images ifft_img, fft_img + c * fft_img_step);
+// src[0] / dst, one stripe, A.chunks >= 2, elems 2 or 4.
+bool chunks_supported(int L);
+// pw: packs per wave (1, 2, 4): each wave transforms its chunks for pw packs
+// with one staging of the chunk's tables (A.packs_per_xcd is recomputed).
+hipError_t launch_chunks(int L, bool high, const MonoCore &A, hipStream_t stream, int pw = 1);
 // kMonoHalf* modes: L = 11 only, one stripe, grid.y = halves (launch_mono_half).
 hipError_t launch_mono_half(int mode, uint32_t halves, const MonoArgs &A, hipStream_t stream);
 // Variant launch_mono picks: LDS-staged twiddles (single chunk, 2 rows per

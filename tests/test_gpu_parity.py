@@ -955,6 +955,65 @@ def test_lane_kernel_encode_matches_oracle(torch, rs, rate, N, M, S):
 
 
 # ---------------------------------------------------------------------------
+# multi-chunk encodes of 2^2..2^7-row transforms in one launch (rs_chunks.hip k_chunks): the
+# waves of a pack's workgroup take HighRate input chunks / LowRate output chunks in parallel
+# (routed by default for HighRate with <= 8 chunks; rs_mono_enable + 512 forces every shape)
+
+CHUNKS_CASES = [
+    # (rate, N, M, S): HighRate N > pow2(M) (chunks = ceil(N / pow2(M))), LowRate M > pow2(N)
+    ("high", 1000, 100, 1024), ("high", 1000, 128, 256), ("high", 2000, 100, 192), ("high", 500, 64, 130),
+    ("high", 300, 30, 64), ("high", 100, 10, 6), ("high", 50, 5, 64), ("high", 20, 3, 2), ("high", 9000, 100, 2),
+    ("low", 128, 1024, 1024), ("low", 100, 1000, 256), ("low", 64, 640, 130), ("low", 10, 100, 64),
+    ("low", 3, 20, 6), ("low", 100, 9000, 2), ("default", 4000, 120, 64), ("default", 5, 41, 320),
+]
+
+
+@pytest.mark.parametrize("mono", [1 | 512, 1 | 8 | 512, 1 | 16 | 512])
+@pytest.mark.parametrize("rate,N,M,S", CHUNKS_CASES)
+def test_chunks_kernel_encode_matches_oracle(torch, rs, rate, N, M, S, mono):
+    rs.mono_enable(mono)
+    try:
+        orig = O.generate_original(N, S, (3 * N + M + S) & 0xFF)
+        want = O.encode(rate, orig, M)
+        d_o = _dev(torch, orig)
+        d_r = torch.full((M, S), 0xEE, dtype=torch.uint8, device="cuda")
+        route = _route_of(torch, rs, lambda: rs.encode_device(N, M, S, d_o, d_r, rate_=RATE[rate]))
+        assert len(route) == 1 and route[0].startswith("k_chunks<"), route
+        assert np.array_equal(d_r.cpu().numpy(), want)
+        # strided rows: column slices of wider matrices
+        wo = torch.full((N, S + 64), 0x11, dtype=torch.uint8, device="cuda")
+        wr = torch.full((M, S + 64), 0x22, dtype=torch.uint8, device="cuda")
+        wo[:, 32:32 + S] = d_o
+        rs.encode_device(N, M, S, wo[:, 32:32 + S], wr[:, 32:32 + S], rate_=RATE[rate])
+        torch.cuda.synchronize()
+        got = wr.cpu().numpy()
+        assert np.array_equal(got[:, 32:32 + S], want)
+        assert np.all(got[:, :32] == 0x22) and np.all(got[:, 32 + S:] == 0x22)
+    finally:
+        rs.mono_enable(1)
+
+
+def test_chunks_kernel_off_matches_on(torch, rs):
+    """rs_mono_enable + 1024 (k_chunks off: the chunk-parallel passes) gives the same bytes as the
+    default route (k_chunks for this HighRate 8-chunk shape)."""
+    N, M, S = 1000, 100, 1024
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    d_o = torch.randint(0, 256, (N, S), dtype=torch.uint8, device="cuda", generator=g)
+    outs = []
+    for mode in (1 | 1024, 1):
+        rs.mono_enable(mode)
+        try:
+            d_r = torch.empty((M, S), dtype=torch.uint8, device="cuda")
+            rs.encode_device(N, M, S, d_o, d_r)
+            torch.cuda.synchronize()
+            outs.append(d_r)
+        finally:
+            rs.mono_enable(1)
+    assert torch.equal(outs[0], outs[1])
+
+
+# ---------------------------------------------------------------------------
 # half-split 2^12-row transforms (rs_codec.cpp half_split, rs_mono_enable + 128; off by
 # default, slower than the passes): two launches of the 2^11-row column kernel -- the IFFT
 # below the top layer per half with input rows, then the top layer (+ the decode's formal

@@ -1,0 +1,120 @@
+// Multi-chunk column kernel timing (development tool): k_chunks (rs_chunks.hip)
+// on one shape, back-to-back launch time and per-workgroup s_memrealtime stamps
+// of wave 0 and the last wave (RS_CHUNK_STAMPS).
+// Build: bash tools/build_chunks_probe.sh   Run: tools/_probe/chunks_probe N M S high|low [e2|e4]
+#ifndef RS_CHUNK_NO_STAMPS
+#define RS_CHUNK_STAMPS 1
+#endif
+#include "../reed-solomon-simd_amd/csrc/rs_chunks.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../reed-solomon-simd_amd/csrc/gf_tables.hpp"
+
+#define CK(x)                                                                        \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                                 \
+        }                                                                            \
+    } while (0)
+
+int main(int argc, char **argv) {
+    if (argc < 5) {
+        fprintf(stderr, "usage: chunks_probe N M S high|low [e2|e4]\n");
+        return 2;
+    }
+    const uint32_t N = atoi(argv[1]), M = atoi(argv[2]), S = atoi(argv[3]);
+    const bool high = std::string(argv[4]) == "high";
+    const bool e2 = argc > 5 ? std::string(argv[5]) == "e2" : S <= 1024;
+    auto p2 = [](uint32_t x) { uint32_t n = 1; while (n < x) n <<= 1; return n; };
+    const uint32_t n = high ? p2(M) : p2(N);
+    uint32_t L = 0;
+    while ((1u << L) < n) ++L;
+    const uint32_t C = high ? (N + n - 1) / n : (M + n - 1) / n;
+    const auto &T = rs::tables();
+    const int tw = e2 ? rs::kPerm2Words : rs::kPermWords;
+    const std::vector<uint32_t> &skew_tabs = e2 ? T.perm2_by_skew : T.perm_by_skew;
+    const uint32_t nimg = 65536u / n;
+    const size_t words = size_t(n - 1) * tw;
+    std::vector<uint32_t> h(words * nimg);
+    for (uint32_t t = 0; t < nimg; ++t)
+        for (uint32_t b = 0; b < L; ++b)
+            for (uint32_t g = 0; g < (n >> (b + 1)); ++g) {
+                const uint32_t slot = n - (n >> b) + g, idx = (g << (b + 1)) + (1u << b) + t * n - 1;
+                std::copy_n(&skew_tabs[size_t(idx) * tw], tw, &h[t * words + size_t(slot) * tw]);
+            }
+    uint32_t *d_img;
+#ifdef RS_CHUNK_REPL
+    const size_t repl_words = (h.size() + 1023) / 1024 * 1024 + 256 * 1024;  // replicas 1 MiB + apart
+    CK(hipMalloc(&d_img, repl_words * 4 * RS_CHUNK_REPL));
+    for (int r = 0; r < RS_CHUNK_REPL; ++r)
+        CK(hipMemcpy(d_img + r * repl_words, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+#else
+    CK(hipMalloc(&d_img, h.size() * 4));
+    CK(hipMemcpy(d_img, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+#endif
+    uint8_t *orig, *rec;
+    CK(hipMalloc(&orig, size_t(N) * S));
+    CK(hipMalloc(&rec, size_t(M) * S));
+    CK(hipMemset(orig, 0x37, size_t(N) * S));
+    rs::MonoCore A;
+    A.elems = e2 ? 2 : 4;
+    A.packs = e2 ? S / 4 : S / 8;
+    A.packs_per_xcd = (A.packs + 7) / 8;
+    A.src[0] = rs::RowMap{orig, S, 0, N};
+    A.nsrc = 1;
+    A.dst = rs::RowMap{rec, S, 0, M};
+    A.chunks = C;
+    A.img = d_img;
+    A.img_words = words;
+    A.ifft_img = high ? 1 : 0;
+    A.ifft_img_step = high ? 1 : 0;
+    A.fft_img = high ? 0 : 1;
+    A.fft_img_step = high ? 0 : 1;
+#ifdef RS_CHUNK_REPL
+    A.end = uint32_t(repl_words);
+#endif
+    const int iters = 1000;
+    const int pw = getenv("PW") ? atoi(getenv("PW")) : 1;
+    auto go = [&] { CK(rs::launch_chunks(int(L), high, A, 0, pw)); };
+    for (int i = 0; i < 20; ++i) go();
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < iters; ++i) go();
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    printf("k_chunks<%u, %d, %s, %d> %u:%u x %u B, %u chunks: %.2f us/launch (back-to-back)\n", L, e2 ? 2 : 4,
+           high ? "high" : "low", pw, N, M, S, C, ms * 1000 / iters);
+#ifdef RS_CHUNK_STAMPS
+    CK(hipDeviceSynchronize());
+    go();
+    CK(hipDeviceSynchronize());
+    const uint32_t wgs = 8 * (((A.packs + pw - 1) / pw + 7) / 8);
+    std::vector<uint64_t> st(4096 * 2 * 8);
+    CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(rs::g_chunk_stamps), st.size() * 8));
+    const char *names[8] = {"entry", "tables written", "transform 1", "loop done", "barrier", "fft done", "stored", ""};
+    for (int w = 0; w < 2; ++w)
+        for (int i = 0; i < 7; ++i) {
+            std::vector<double> v;
+            for (uint32_t g = 0; g < wgs; ++g) {
+                const uint64_t t0 = st[(g * 2 + 0) * 8 + 0], t = st[(g * 2 + w) * 8 + i];
+                if (t && t0) v.push_back((double(t) - double(t0)) * 0.01);
+            }
+            if (v.empty()) continue;
+            std::sort(v.begin(), v.end());
+            printf("%s %-15s min %6.2f  med %6.2f  max %6.2f us\n", w ? "last wave" : "wave 0   ", names[i], v.front(),
+                   v[v.size() / 2], v.back());
+        }
+#endif
+    return 0;
+}
