@@ -102,12 +102,21 @@ template <int L, int E>
 struct CTabs {
     using G = ChunkGeo<L, E>;
     uint4 v[G::KP];
+    uint32_t rot = 0;  // RS_CHUNK_ROT: the workgroup's rotation of the piece order
+    __device__ __forceinline__ uint32_t piece(uint32_t q) const {
+#ifdef RS_CHUNK_ROT
+        const uint32_t r = q + rot;
+        return r < G::pieces ? r : r - G::pieces;
+#else
+        return q;
+#endif
+    }
     __device__ __forceinline__ void issue(const uint32_t *img, uint32_t lane) {
         const uint4 *src = reinterpret_cast<const uint4 *>(img);
         static_for<0, G::KP>([&](auto kc) {
             const uint32_t q = lane + 64u * decltype(kc)::value;
 #ifndef RS_CHUNK_SKIP_TABS  // (tools/chunks_probe.hip ablation)
-            v[kc] = src[q < G::pieces ? q : G::pieces - 1];
+            v[kc] = src[piece(q < G::pieces ? q : G::pieces - 1)];
 #else
             v[kc] = uint4{q, q ^ 1u, q ^ 2u, uint32_t(reinterpret_cast<uintptr_t>(src))};
 #endif
@@ -117,7 +126,8 @@ struct CTabs {
         static_for<0, G::KP>([&](auto kc) {
             const uint32_t q = lane + 64u * decltype(kc)::value;
             if (q < G::pieces) {
-                const uint32_t t = q / G::PC, p = q - t * G::PC;
+                const uint32_t pq = piece(q);
+                const uint32_t t = pq / G::PC, p = pq - t * G::PC;
                 reinterpret_cast<uint4 *>(region)[t * (kSlot / 4) + p] = v[kc];
             }
         });
@@ -280,6 +290,9 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_chunks(const MonoCore A) {
     const uint32_t W = blockDim.x >> 6;
     uint32_t *region = lds + wave * G::region;
     CTabs<L, E> tabs;
+#ifdef RS_CHUNK_ROT  // (tools/chunks_probe.hip experiment: workgroups start their image reads at different pieces)
+    tabs.rot = (pg * RS_CHUNK_ROT) % G::pieces;
+#endif
     RS_CSTAMP(0);
 #ifdef RS_CHUNK_REPL  // (tools/chunks_probe.hip experiment: RS_CHUNK_REPL image replicas, A.end words apart)
     const uint32_t *img_base = A.img + uint64_t(pg % RS_CHUNK_REPL) * A.end;
