@@ -332,11 +332,12 @@ rs_status rs_check_device(rs_context *ctx);
  * none.  Adding 128 runs single-chunk transforms of 2^12 rows as two launches
  * of the 2^11-row kernel split by halves of the rows (off by default: slower
  * than the pass kernels; RS_MI355X_HALF=1 at context creation: on), adding 256
- * turns that off again.  HighRate encodes of 2^2 .. 2^7-row transforms with
- * 2 .. 8 chunks (N > pow2(M)) run as one launch whose waves take the chunks in
- * parallel (rs_chunks.hip; RS_MI355X_CHUNKS=0 at context creation: never):
- * adding 512 sends every multi-chunk encode of those sizes there (LowRate
- * output chunks too), adding 1024 none.
+ * turns that off again.  Multi-chunk encodes of 2^2 .. 2^7-row transforms
+ * (HighRate N > pow2(M), LowRate M > pow2(N)) run as one launch whose waves
+ * take the chunks in parallel (rs_chunks.hip; RS_MI355X_CHUNKS=0 at context
+ * creation: never) where that measured faster: 2-element packs, HighRate or up
+ * to 8 LowRate output chunks; 4-element packs, HighRate up to 8 chunks.  Adding
+ * 512 sends every multi-chunk encode of those sizes there, adding 1024 none.
  * A/B and tests; results are identical in every mode. */
 rs_status rs_mono_enable(rs_context *ctx, int enable);
 

@@ -17,10 +17,12 @@
 // another, or one launch per step with the chunks over the grid -- take
 // 13-30 us for 1000:100 x 1 KiB, profiles/r05g.)
 //
-// Twiddles: each wave stages its chunk's layer-ordered image (the same images
-// as k_mono, rs_codec.cpp mono_images: table of layer b, group g at slot
+// Twiddles: each wave stages its chunk's layer-ordered image (the layout of
+// k_mono's images, rs_codec.cpp mono_images: table of layer b, group g at slot
 // n - n / 2^b + g) into a wave-private LDS region of 20-word slots (16 lanes'
-// ds_read_b128 of 16 different slots then hit 16 different bank groups).
+// ds_read_b128 of 16 different slots then hit 16 different bank groups).  With
+// 2-element packs the images hold 8-word basis tables, expanded while staging
+// (CTabsBasis); 4-element packs stage the 20-word tables.
 //
 // Placement of a wave's n rows: lane l, register k.  Before IFFT layer b the
 // register bit holds row bit b, lane bits j < b row bits j, lane bits j >= b row
@@ -31,6 +33,7 @@
 
 #include <atomic>
 #include <cstdio>
+#include <type_traits>
 
 #include "rs_device.hpp"
 #include "rs_gf.hpp"
@@ -102,21 +105,12 @@ template <int L, int E>
 struct CTabs {
     using G = ChunkGeo<L, E>;
     uint4 v[G::KP];
-    uint32_t rot = 0;  // RS_CHUNK_ROT: the workgroup's rotation of the piece order
-    __device__ __forceinline__ uint32_t piece(uint32_t q) const {
-#ifdef RS_CHUNK_ROT
-        const uint32_t r = q + rot;
-        return r < G::pieces ? r : r - G::pieces;
-#else
-        return q;
-#endif
-    }
     __device__ __forceinline__ void issue(const uint32_t *img, uint32_t lane) {
         const uint4 *src = reinterpret_cast<const uint4 *>(img);
         static_for<0, G::KP>([&](auto kc) {
             const uint32_t q = lane + 64u * decltype(kc)::value;
 #ifndef RS_CHUNK_SKIP_TABS  // (tools/chunks_probe.hip ablation)
-            v[kc] = src[piece(q < G::pieces ? q : G::pieces - 1)];
+            v[kc] = src[q < G::pieces ? q : G::pieces - 1];
 #else
             v[kc] = uint4{q, q ^ 1u, q ^ 2u, uint32_t(reinterpret_cast<uintptr_t>(src))};
 #endif
@@ -126,9 +120,57 @@ struct CTabs {
         static_for<0, G::KP>([&](auto kc) {
             const uint32_t q = lane + 64u * decltype(kc)::value;
             if (q < G::pieces) {
-                const uint32_t pq = piece(q);
-                const uint32_t t = pq / G::PC, p = pq - t * G::PC;
+                const uint32_t t = q / G::PC, p = q - t * G::PC;
                 reinterpret_cast<uint4 *>(region)[t * (kSlot / 4) + p] = v[kc];
+            }
+        });
+    }
+};
+
+// 2-element tables built in the kernel from their basis images (rs_codec.cpp
+// basis_images): per table the 16 products P(e_i) = x * e_i of the multiplier with
+// the Cantor basis elements, 8 words (word 2f = P(e_2f) | P(e_2f+1) << 16 for the
+// low byte's 2-bit field f, word 2f + 1 the high byte's) -- half the bytes of the
+// 16-word table.  Multiplication by a constant is GF(2)-linear, so field f's four
+// lookups are {0, a, b, a ^ b} (a, b its two basis products): a word X = a | b << 16
+// gives the table words [0, a_lo, b_lo, (a ^ b)_lo] and [0, a_hi, b_hi, (a ^ b)_hi]
+// (gf_tables.cpp fill_perm2) by two v_perm_b32 each.  1000:100 x 1 KiB 10.8 -> 5.9 us
+// per launch against staging the 16-word images (profiles/r05g/chunks_basis.txt):
+// the staging's L2 requests, not the 32 VALU per table, bound the launch.
+template <int L>
+struct CTabsBasis {
+    static constexpr uint32_t n = 1u << L, tabs = n - 1;
+    static constexpr int KT = int((tabs + 63) / 64);  // tables per lane
+    uint4 v[KT][2];
+    __device__ __forceinline__ void issue(const uint32_t *img, uint32_t lane) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(img);
+        static_for<0, KT>([&](auto kc) {
+            const uint32_t t = lane + 64u * decltype(kc)::value, tt = t < tabs ? t : tabs - 1;
+            v[kc][0] = src[2 * tt];
+            v[kc][1] = src[2 * tt + 1];
+        });
+    }
+    __device__ __forceinline__ void write(uint32_t *region, uint32_t lane) const {
+        static_for<0, KT>([&](auto kc) {
+            const uint32_t t = lane + 64u * decltype(kc)::value;
+            if (t < tabs) {
+                const uint32_t X[8] = {v[kc][0].x, v[kc][0].y, v[kc][0].z, v[kc][0].w,
+                                       v[kc][1].x, v[kc][1].y, v[kc][1].z, v[kc][1].w};
+                uint32_t w[16];
+                static_for<0, 4>([&](auto fc) {
+                    constexpr int f = decltype(fc)::value;
+                    const uint32_t A = X[2 * f], C = X[2 * f + 1];
+                    const uint32_t tA = A ^ __builtin_amdgcn_alignbit(A, A, 16), tC = C ^ __builtin_amdgcn_alignbit(C, C, 16);
+                    w[4 * f + 0] = __builtin_amdgcn_perm(tA, A, 0x0402000Cu);  // direct: low-byte field, low bytes
+                    w[4 * f + 1] = __builtin_amdgcn_perm(tC, C, 0x0503010Cu);  // direct: high-byte field, high bytes
+                    w[4 * f + 2] = __builtin_amdgcn_perm(tC, C, 0x0402000Cu);  // cross: high-byte field, low bytes
+                    w[4 * f + 3] = __builtin_amdgcn_perm(tA, A, 0x0503010Cu);  // cross: low-byte field, high bytes
+                });
+                uint4 *d = reinterpret_cast<uint4 *>(region) + t * (kSlot / 4);
+                static_for<0, 4>([&](auto qc) {
+                    constexpr int q = decltype(qc)::value;
+                    d[q] = uint4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+                });
             }
         });
     }
@@ -289,16 +331,9 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_chunks(const MonoCore A) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t W = blockDim.x >> 6;
     uint32_t *region = lds + wave * G::region;
-    CTabs<L, E> tabs;
-#ifdef RS_CHUNK_ROT  // (tools/chunks_probe.hip experiment: workgroups start their image reads at different pieces)
-    tabs.rot = (pg * RS_CHUNK_ROT) % G::pieces;
-#endif
+    std::conditional_t<E == 2, CTabsBasis<L>, CTabs<L, E>> tabs;  // (E = 2: basis images)
     RS_CSTAMP(0);
-#ifdef RS_CHUNK_REPL  // (tools/chunks_probe.hip experiment: RS_CHUNK_REPL image replicas, A.end words apart)
-    const uint32_t *img_base = A.img + uint64_t(pg % RS_CHUNK_REPL) * A.end;
-#else
     const uint32_t *img_base = A.img;
-#endif
     if constexpr (HIGH) {
         // chunk c: IFFT with skew offset c n + n (image ifft_img + c), XOR-folded
         CRows<PW> acc;

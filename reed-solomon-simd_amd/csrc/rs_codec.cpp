@@ -229,6 +229,7 @@ struct rs_context {
     std::mutex img_mu;            // guards d_img, d_img2
     uint32_t *d_img[13] = {};     // column-kernel twiddle images per L (built at context creation)
     uint32_t *d_img2[13] = {};    // the same in the 2-element table format
+    uint32_t *d_imgb[13] = {};    // 8-word basis images of the 2-element format (basis_images)
     std::mutex host_engine_mu;  // guards host_engine_buf (rs_engine_*_host staging)
     DevBuf host_engine_buf;
     std::mutex mu;  // guards ws_by_stream (device-resident API scratch), prof, recs
@@ -520,6 +521,41 @@ const uint32_t *mono_images(rs_context *ctx, uint32_t L, uint32_t elems = 4) {
     return d;
 }
 
+// Basis images (the 2-element staged kernels' twiddles: k_mono, rs_mono.hip
+// basis_expand, and k_chunks): the layout of mono_images, 8 words per table -- the
+// products P(e_i) = x * e_i of the table's multiplier with the 16 Cantor basis
+// elements, word 2f = P(e_2f) | P(e_2f+1) << 16 (the low byte's 2-bit field f),
+// word 2f + 1 = P(e_8+2f) | P(e_9+2f) << 16 (the high byte's); zero for skew 65535.
+constexpr uint32_t kBasisWords = 8;
+const uint32_t *basis_images(rs_context *ctx, uint32_t L) {
+    std::lock_guard<std::mutex> lock(ctx->img_mu);
+    uint32_t *&slot_ptr = ctx->d_imgb[L];
+    if (slot_ptr) return slot_ptr;
+    const rs::GfTables &T = rs::tables();
+    const uint32_t n = 1u << L, nimg = 65536u / n;
+    const size_t words = size_t(n - 1) * kBasisWords;
+    std::vector<uint32_t> h(words * nimg);
+    for (uint32_t t = 0; t < nimg; ++t) {
+        uint32_t *dst = &h[t * words];
+        for (uint32_t b = 0; b < L; ++b)
+            for (uint32_t g = 0; g < (n >> (b + 1)); ++g) {
+                const uint32_t slot = n - (n >> b) + g;
+                const uint32_t idx = (g << (b + 1)) + (1u << b) + t * n - 1;
+                const uint16_t lm = T.skew[idx];
+                auto P = [&](int i) -> uint32_t { return lm == 65535 ? 0u : T.mul(uint16_t(1u << i), lm); };
+                for (uint32_t f = 0; f < 4; ++f) {
+                    dst[size_t(slot) * kBasisWords + 2 * f] = P(int(2 * f)) | (P(int(2 * f + 1)) << 16);
+                    dst[size_t(slot) * kBasisWords + 2 * f + 1] = P(int(8 + 2 * f)) | (P(int(9 + 2 * f)) << 16);
+                }
+            }
+    }
+    uint32_t *d = nullptr;
+    check(hipMalloc(&d, h.size() * 4));
+    check(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    slot_ptr = d;
+    return d;
+}
+
 // The column kernel runs where it beats the pass kernels: its staged
 // variant (one chunk, L <= 10).  RS_MI355X_MONO_ALL=1 also routes multi-chunk
 // and L = 11, 12 transforms to its unstaged variant (tests, tuning).
@@ -546,8 +582,10 @@ rs::MonoArgs mono_args(rs_context *ctx, uint32_t L, const Geom &g, bool staged, 
                   : g.fmt.full_packs == 0xFFFFFFFFu ? 2 * g.packs : 2 * g.fmt.full_packs + (g.fmt.tail_h + 1) / 2;
     M.packs_per_xcd = (M.packs + 7) / 8;
     M.stripes = g.stripes;  // a batch of stripes runs in one launch
-    M.img = mono_images(ctx, L, M.elems);
-    M.img_words = uint64_t((1u << L) - 1) * (e2 ? rs::kPerm2Words : rs::kPermWords);
+    // 2-element packs with RS_MONO_BASIS: basis images (rs_mono.hip Stage::kBasis builds the tables)
+    const bool basis = e2 && RS_MONO_BASIS;
+    M.img = basis ? basis_images(ctx, L) : mono_images(ctx, L, M.elems);
+    M.img_words = uint64_t((1u << L) - 1) * (basis ? kBasisWords : e2 ? rs::kPerm2Words : rs::kPermWords);
     M.lut = e2 ? ctx->d_lut2 : ctx->d_lut;
     M.fmt = g.fmt;
     return M;
@@ -565,30 +603,41 @@ void launch_mono(int mode, uint32_t L, const rs::MonoArgs &M, hipStream_t s, uin
 bool try_lane(rs_context *ctx, uint32_t L, uint32_t chunks, const rs::MonoArgs &M, hipStream_t s, uint64_t bytes) {
     if (!ctx->lane || chunks != 1 || M.elems != 2 || int(L) > ctx->lane_max_l || !rs::lane_supported(int(L)))
         return false;
+    rs::MonoArgs F = M;  // the lane kernel stages the 16-word tables
+    F.img = mono_images(ctx, L, 2);
+    F.img_words = uint64_t((1u << L) - 1) * rs::kPerm2Words;
     hipEvent_t ev = nullptr;
     if (t_prof_ctx) prof_begin(s, &ev);
-    check(rs::launch_lane(int(L), M, s));
+    check(rs::launch_lane(int(L), F, s));
     if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), bytes);
     return true;
 }
 
 // Multi-chunk encodes of small transforms (rs_chunks.hip): one launch in which the
 // waves of a pack's workgroup take the chunks in parallel (HighRate input chunks,
-// LowRate output chunks).  One stripe; the column kernel's pack bound.  Routed
-// by default where it measured faster than the passes (profiles/r05g): HighRate
-// with at most one chunk per wave (1000:100 x 1 KiB 13.2 -> 10.9 us, 500:64 10.3 ->
-// 7.8, 100:10 18.5 -> 8.6); LowRate (one pass, the output chunks over the grid) and
-// more chunks than waves stay on the passes unless forced (rs_mono_enable + 512).
+// LowRate output chunks).  One stripe; the column kernel's pack bound.  Routed by
+// default where it measured faster than the passes (profiles/r05h/chunks_*.jsonl,
+// wall us per call at 1 KiB shards): with 2-element packs (basis tables) every
+// HighRate shape (1000:100 13.2 -> 6.5, 9000:100 35.2 -> 21.1, 100:10 7.9 -> 4.9) and
+// LowRate up to 8 output chunks (128:1024 8.2 -> 6.2; 64:640 and 100:9000, one pass
+// with the chunks over the grid, tie or win); with 4-element packs (20-word tables)
+// HighRate up to 8 chunks (1000:100 x 2 KiB 13.1 -> 12.3; LowRate 128:1024 x 2 KiB
+// 8.5 -> 11.4 stays on the pass).  rs_mono_enable + 512 / RS_MI355X_CHUNKS=2: every shape.
 bool use_chunks(rs_context *ctx, uint32_t L, const Geom &g, uint32_t chunks, bool high) {
     // (RS_MI355X_CHUNK_PARALLEL forces one of the pass forms: tests, A/B)
     if (!ctx->chunks || !ctx->mono || ctx->mono_all || ctx->chunk_par >= 0 || chunks < 2 || g.stripes != 1 ||
         !rs::chunks_supported(int(L)) || g.packs > ctx->mono_max_packs)
         return false;
-    return ctx->chunks_forced || (high && chunks <= kChunksMaxWaves);
+    const bool e2 = ctx->e2_encode && uint64_t(g.packs) <= ctx->e2_max_packs;  // as mono_args decides
+    return ctx->chunks_forced || (e2 ? high || chunks <= kChunksMaxWaves : high && chunks <= kChunksMaxWaves);
 }
 void launch_chunks(rs_context *ctx, const Geom &g, bool high, uint32_t L, const rs::RowMap &src, const rs::RowMap &dst,
                    uint32_t chunks, uint64_t bytes, hipStream_t s) {
     rs::MonoArgs Mo = mono_args(ctx, L, g, true);
+    if (Mo.elems == 2) {  // 2-element packs: basis images, expanded in the kernel (rs_chunks.hip CTabsBasis)
+        Mo.img = basis_images(ctx, L);
+        Mo.img_words = uint64_t((1u << L) - 1) * kBasisWords;
+    }
     Mo.src[0] = src;
     Mo.nsrc = 1;
     Mo.dst = dst;
@@ -1449,7 +1498,10 @@ rs_status rs_context_create(int device, rs_context **out) {
         ctx->lane_default = ctx->lane;
         if (const char *hs = getenv("RS_MI355X_HALF")) ctx->half = hs[0] == '1';
         ctx->half_default = ctx->half;
-        if (const char *ck = getenv("RS_MI355X_CHUNKS")) ctx->chunks = ck[0] == '1';
+        if (const char *ck = getenv("RS_MI355X_CHUNKS")) {  // 0 off, 1 default routing, 2 every supported shape
+            ctx->chunks = ck[0] != '0';
+            ctx->chunks_forced = ck[0] == '2';
+        }
         ctx->chunks_default = ctx->chunks;
         {  // top_table: skew index 2047 + 2048 j, both table formats
             std::vector<uint32_t> top(size_t(kTopTables) * (rs::kPermWords + rs::kPerm2Words));
@@ -1484,6 +1536,7 @@ rs_status rs_context_create(int device, rs_context **out) {
         // synchronous upload the first time a size is seen
         for (uint32_t L = kChunksMinL; L <= kMonoMaxL; ++L) mono_images(ctx, L);
         for (uint32_t L = kChunksMinL; L <= 11; ++L) mono_images(ctx, L, 2);
+        for (uint32_t L = kChunksMinL; L <= (RS_MONO_BASIS ? 11u : 7u); ++L) basis_images(ctx, L);
         return RS_OK;
     });
     if (st != RS_OK) {
@@ -1504,6 +1557,8 @@ void rs_context_destroy(rs_context *ctx) {
     if (ctx->d_lut2) (void)hipFree(ctx->d_lut2);
     if (ctx->d_top) (void)hipFree(ctx->d_top);
     for (uint32_t *p : ctx->d_img2)
+        if (p) (void)hipFree(p);
+    for (uint32_t *p : ctx->d_imgb)
         if (p) (void)hipFree(p);
     if (ctx->d_lwfold_base) (void)hipFree(ctx->d_lwfold_base);
     for (uint32_t *p : ctx->d_img)

@@ -188,6 +188,13 @@ char *launch_name_buf();
 // layer-ordered images: image t (transform skew offset t * n) holds, for
 // layer b = 0..L-1 and group g < n / 2^(b+1), the perm table of skew index
 // g * 2^(b+1) + 2^b + t * n - 1 at table slot n - n / 2^b + g.
+// 2-element staged column kernels (k_mono) stage 8-word basis images and build
+// their tables in LDS (rs_mono.hip Stage::kBasis) when 1; the host (rs_codec.cpp
+// mono_args) hands them the matching images.  Measured no faster there, so 0;
+// k_chunks always uses basis images for 2-element packs.
+#ifndef RS_MONO_BASIS
+#define RS_MONO_BASIS 0
+#endif
 enum MonoMode {
     kMonoEncodeHigh = 0,
     kMonoEncodeLow = 1,

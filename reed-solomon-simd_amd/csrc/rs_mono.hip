@@ -320,12 +320,51 @@ struct GlobalTabs {
     }
 };
 
+// Basis images (2-element packs, RS_MONO_BASIS, default off): the staging loads a
+// table's 16 basis products (8 words, rs_codec.cpp basis_images) instead of its 16
+// words, and builds the table in LDS.  Multiplication by a constant is GF(2)-linear,
+// so the four lookups of 2-bit field f are {0, a, b, a ^ b} with a, b its two basis
+// products; basis word 2f = a | b << 16 of the low byte's field f (A_f), word 2f + 1
+// the high byte's (C_f), so one 16-byte basis piece (A_f, C_f, A_f+1, C_f+1) makes
+// table pieces f and f + 1 (gf_tables.cpp fill_perm2: direct words [0, a_lo, b_lo,
+// (a^b)_lo] and [0, c_hi, d_hi, (c^d)_hi], cross words with the other bytes), two
+// v_perm_b32 and an XOR per word pair.  Half the staging's L2 requests: k_chunks
+// 1000:100 x 1 KiB 10.8 -> 5.9 us per launch (profiles/r05g/chunks_basis.txt), but
+// k_mono unchanged or slower: headline encode 7.92 / 7.96 -> 7.94 / 7.94 us, decode
+// 2^11 rows 1 % 13.47 / 13.42 -> 13.63 / 13.62 us (profiles/r05h/basis_ab.txt), so
+// RS_MONO_BASIS (rs_device.hpp) is off: 1 builds k_mono with it (the host then
+// hands it basis images, rs_codec.cpp mono_args).
+__device__ __forceinline__ void basis_expand(const uint4 &v, uint4 &a, uint4 &b) {
+    auto field = [](uint32_t A, uint32_t C) {
+        const uint32_t tA = A ^ __builtin_amdgcn_alignbit(A, A, 16), tC = C ^ __builtin_amdgcn_alignbit(C, C, 16);
+        return uint4{__builtin_amdgcn_perm(tA, A, 0x0402000Cu), __builtin_amdgcn_perm(tC, C, 0x0503010Cu),
+                     __builtin_amdgcn_perm(tC, C, 0x0402000Cu), __builtin_amdgcn_perm(tA, A, 0x0503010Cu)};
+    };
+    a = field(v.x, v.y);
+    b = field(v.z, v.w);
+}
+
 template <int L, int LR, int SP = 0, int E = 4>
 struct Stage {
     static constexpr bool SPLIT = Plan<L, LR, SP>::SPLIT;
     static constexpr int FLO = Plan<L, LR, SP>::FLO;
     static constexpr int TW = Fmt<E>::kTW;
     static constexpr uint32_t PC = Fmt<E>::kPC;
+    static constexpr bool kBasis = E == 2 && RS_MONO_BASIS;
+    static constexpr uint32_t LPC = kBasis ? 2 : PC;  // image pieces per table (basis images: 8 words)
+    // write image piece q (of a region's image pieces) into the region's LDS slots
+    template <typename AT>
+    static __device__ __forceinline__ void put(uint32_t *region, uint32_t q, const uint4 &v, AT at) {
+        if constexpr (kBasis) {
+            const uint32_t p0 = (q >> 1) * PC + (q & 1u) * 2u;  // table piece of field 2 (q & 1)
+            uint4 a, b;
+            basis_expand(v, a, b);
+            reinterpret_cast<uint4 *>(region)[at(p0)] = a;
+            reinterpret_cast<uint4 *>(region)[at(p0 + 1)] = b;
+        } else {
+            reinterpret_cast<uint4 *>(region)[at(q)] = v;
+        }
+    }
     // LDS slot of a table: 20 words in both formats.  A 2-element table is 16
     // words, and slots of 16 words (64 B, a quarter of the banks) would put lanes
     // that read tables t and t + 4 on the same banks; 20-word slots cycle through
@@ -1305,31 +1344,32 @@ __device__ __forceinline__ void col_eval_poly(const MonoCore &A, uint32_t ebits,
 template <int L, int LR, int SPLIT, int E>
 __device__ __forceinline__ uint4 priv_piece(const uint32_t *img, uint32_t wave, uint32_t q) {
     using G = Stage<L, LR, SPLIT, E>;
-    const uint32_t t = q / G::PC, piece = q - t * G::PC;
+    const uint32_t t = q / G::LPC, piece = q - t * G::LPC;
     const uint32_t y = (G::W >> G::B0) - t;                   // in [1, W >> B0]
     const int b = G::IW - int(32 - __builtin_clz(y - 1));    // IW - ceil(log2 y)
     const uint32_t local = t - ((G::W >> G::B0) - (G::W >> b));
     const uint32_t slot = G::n - (G::n >> b) + wave * (G::W >> (b + 1)) + local;
-    return reinterpret_cast<const uint4 *>(img)[slot * G::PC + piece];
+    return reinterpret_cast<const uint4 *>(img)[slot * G::LPC + piece];
 }
 // 16-byte piece q of the layer-0 tables of wave `wave`'s phase-1 / -3 rows
 // (image slots wave * W/2 .. : contiguous, one coalesced read per wave)
 template <int L, int LR, int SPLIT, int E>
 __device__ __forceinline__ uint4 l0_piece(const uint32_t *img, uint32_t wave, uint32_t q) {
     using G = Stage<L, LR, SPLIT, E>;
-    return reinterpret_cast<const uint4 *>(img)[wave * G::kL0 * G::PC + q];
+    return reinterpret_cast<const uint4 *>(img)[wave * G::kL0 * G::LPC + q];
 }
 template <int L, int LR, int SPLIT, int E>
 __device__ __forceinline__ const uint4 *shared_piece_ptr(const uint32_t *img_i, const uint32_t *img_f, uint32_t q) {
     using G = Stage<L, LR, SPLIT, E>;
-    const uint32_t t = q / G::PC, piece = q - t * G::PC;
+    const uint32_t t = q / G::LPC, piece = q - t * G::LPC;
     const uint32_t slot = t < G::kShI ? G::n - (G::n >> G::IW) + t : G::n - (G::n >> G::FLO) + (t - G::kShI);
-    return reinterpret_cast<const uint4 *>(t < G::kShI ? img_i : img_f) + slot * G::PC + piece;
+    return reinterpret_cast<const uint4 *>(t < G::kShI ? img_i : img_f) + slot * G::LPC + piece;
 }
 // 16-byte piece q of the D tables (Stage::kD): layer b = q / PC of image t_i ^ t_f, group 0
 template <int L, int LR, int SPLIT, int E>
 __device__ __forceinline__ const uint4 *d_piece_ptr(const uint32_t *img_d, uint32_t q) {
     using G = Stage<L, LR, SPLIT, E>;
+    static_assert(!G::kBasis, "D tables: full-table images");
     const uint32_t b = q / G::PC, piece = q - b * G::PC;
     return reinterpret_cast<const uint4 *>(img_d) + (G::n - (G::n >> b)) * G::PC + piece;
 }
@@ -1521,10 +1561,13 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             uint32_t *priv = shared + kSh * G::SW + wave * G::kPriv * G::SW;
             uint32_t *rinfo = lds + G::words;  // decode with fused eval_poly
             constexpr uint32_t PC = G::PC;  // 16-byte pieces per table
-            constexpr int KP1 = (PC * G::kUp + 63) / 64;
-            constexpr int KP0 = G::B0 ? (PC * G::kL0 + 63) / 64 : 1;
-            constexpr int KP3 = G::kP3 ? (PC * G::kP3 + 63) / 64 : 1;  // (guarded by q < PC * kP3)
-            constexpr int KSH = kSh ? (PC * kSh + T - 1) / T : 1;  // (guarded by q < PC * kSh)
+            // image pieces per table: PC, or 2 with basis images (Stage::put builds the tables)
+            constexpr uint32_t LPC = G::LPC;
+            static_assert(!(G::kBasis && kDerive3), "derived phase-3 tables: full-table images");
+            constexpr int KP1 = (LPC * G::kUp + 63) / 64;
+            constexpr int KP0 = G::B0 ? (LPC * G::kL0 + 63) / 64 : 1;
+            constexpr int KP3 = G::kP3 ? (LPC * G::kP3 + 63) / 64 : 1;  // (guarded by q < LPC * kP3)
+            constexpr int KSH = kSh ? (LPC * kSh + T - 1) / T : 1;  // (guarded by q < LPC * kSh)
             RS_MSTAMP(0);
             // decode: does this wave's phase-1 row block (2^IW consecutive rows) hold a
             // received row?  If not its rows are zero through phase 1: it loads no
@@ -1594,12 +1637,12 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
 #ifndef RS_MONO_SKIP_STAGE  // tools/mono_probe.hip ablation
                 if constexpr (G::B0)
                     static_for<0, KP0>([&](auto kc) {
-                        const uint32_t q = clamp_piece(lane + 64u * decltype(kc)::value, PC * G::kL0);
-                        v0[kc] = l0_piece<L, LR, PK, E>(img_i, wave, live ? q : q % PC);
+                        const uint32_t q = clamp_piece(lane + 64u * decltype(kc)::value, LPC * G::kL0);
+                        v0[kc] = l0_piece<L, LR, PK, E>(img_i, wave, live ? q : q % LPC);
                     });
                 static_for<0, KP1>([&](auto kc) {
-                    const uint32_t q = clamp_piece(lane + 64u * decltype(kc)::value, PC * G::kUp);
-                    v1[kc] = priv_piece<L, LR, PK, E>(img_i, wave, live ? q : q % PC);
+                    const uint32_t q = clamp_piece(lane + 64u * decltype(kc)::value, LPC * G::kUp);
+                    v1[kc] = priv_piece<L, LR, PK, E>(img_i, wave, live ? q : q % LPC);
                 });
 #endif
             };
@@ -1608,7 +1651,7 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
 #ifndef RS_MONO_SKIP_STAGE
                 if constexpr (kSh > 0)
                     static_for<0, KSH>([&](auto kc) {
-                        const uint32_t q = clamp_piece(threadIdx.x + T * decltype(kc)::value, PC * kSh);
+                        const uint32_t q = clamp_piece(threadIdx.x + T * decltype(kc)::value, LPC * kSh);
                         if constexpr (kSh == G::kShared) {
                             vs[kc] = ld_piece(shared_piece_ptr<L, LR, PK, E>(img_i, img_f, q));
                         } else {
@@ -1688,7 +1731,7 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
 #ifndef RS_MONO_SKIP_STAGE
                 static_for<0, KP1>([&](auto kc) {
                     const uint32_t q = lane + 64u * decltype(kc)::value;
-                    if (q < PC * G::kUp) reinterpret_cast<uint4 *>(priv)[G::at1(q)] = v1[kc];
+                    if (q < LPC * G::kUp) G::put(priv, q, v1[kc], [](uint32_t p) { return G::at1(p); });
                 });
 #endif
             };
@@ -1697,14 +1740,14 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 if constexpr (G::B0 && !HALF_F)
                     static_for<0, KP0>([&](auto kc) {
                         const uint32_t q = lane + 64u * decltype(kc)::value;
-                        if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at0(q)] = v0[kc];
+                        if (q < LPC * G::kL0) G::put(priv, q, v0[kc], [](uint32_t p) { return G::at0(p); });
                     });
                 else
                     write1();
             }
             static_for<0, KSH>([&](auto kc) {
                 const uint32_t q = threadIdx.x + T * decltype(kc)::value;
-                if (q < PC * kSh) reinterpret_cast<uint4 *>(shared)[G::atS(q)] = vs[kc];
+                if (q < LPC * kSh) G::put(shared, q, vs[kc], [](uint32_t p) { return G::atS(p); });
             });
 #endif
             C cb;  // kMonoHalfF: the upper half's rows
@@ -1724,8 +1767,8 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 if constexpr (G::kP3 > 0)
                 static_for<0, KP3>([&](auto kc) {
                     const uint32_t q = lane + 64u * decltype(kc)::value;
-                    const uint32_t qc = clamp_piece(q, PC * G::kP3);
-                    v3[kc] = priv_piece<L, LR, PK, E>(img_f, wave, out_wave ? qc : qc % PC);
+                    const uint32_t qc = clamp_piece(q, LPC * G::kP3);
+                    v3[kc] = priv_piece<L, LR, PK, E>(img_f, wave, out_wave ? qc : qc % LPC);
                 });
             };
             auto write3 = [&]() {
@@ -1751,7 +1794,7 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 }
                 static_for<0, KP3>([&](auto kc) {
                     const uint32_t q = lane + 64u * decltype(kc)::value;
-                    if (q < PC * G::kP3) reinterpret_cast<uint4 *>(priv)[G::at1(q)] = v3[kc];
+                    if (q < LPC * G::kP3) G::put(priv, q, v3[kc], [](uint32_t p) { return G::at1(p); });
                 });
             };
             // B0: the FFT's layer-0 tables (phase 3's last layer), requested while the
@@ -1761,15 +1804,15 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 if constexpr (G::B0)
                     static_for<0, KP0>([&](auto kc) {
                         const uint32_t q = lane + 64u * decltype(kc)::value;
-                        const uint32_t qc = clamp_piece(q, PC * G::kL0);
-                        v4[kc] = l0_piece<L, LR, PK, E>(img_f, wave, need ? qc : qc % PC);
+                        const uint32_t qc = clamp_piece(q, LPC * G::kL0);
+                        v4[kc] = l0_piece<L, LR, PK, E>(img_f, wave, need ? qc : qc % LPC);
                     });
             };
             auto write4 = [&]() {
                 if constexpr (G::B0)
                     static_for<0, KP0>([&](auto kc) {
                         const uint32_t q = lane + 64u * decltype(kc)::value;
-                        if (q < PC * G::kL0) reinterpret_cast<uint4 *>(priv)[G::at0(q)] = v4[kc];
+                        if (q < LPC * G::kL0) G::put(priv, q, v4[kc], [](uint32_t p) { return G::at0(p); });
                     });
             };
             // 2-element decodes: the reveal tables are requested just before the FFT's

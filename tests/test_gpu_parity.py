@@ -957,7 +957,8 @@ def test_lane_kernel_encode_matches_oracle(torch, rs, rate, N, M, S):
 # ---------------------------------------------------------------------------
 # multi-chunk encodes of 2^2..2^7-row transforms in one launch (rs_chunks.hip k_chunks): the
 # waves of a pack's workgroup take HighRate input chunks / LowRate output chunks in parallel
-# (routed by default for HighRate with <= 8 chunks; rs_mono_enable + 512 forces every shape)
+# (routed by default where it measured faster, rs_codec.cpp use_chunks; rs_mono_enable + 512
+# forces every shape; 2-element packs stage 8-word basis tables, CTabsBasis)
 
 CHUNKS_CASES = [
     # (rate, N, M, S): HighRate N > pow2(M) (chunks = ceil(N / pow2(M))), LowRate M > pow2(N)

@@ -41,28 +41,37 @@ int main(int argc, char **argv) {
     const int tw = e2 ? rs::kPerm2Words : rs::kPermWords;
     const std::vector<uint32_t> &skew_tabs = e2 ? T.perm2_by_skew : T.perm_by_skew;
     const uint32_t nimg = 65536u / n;
-    const size_t words = size_t(n - 1) * tw;
+    const size_t words = size_t(n - 1) * (e2 ? 8 : tw);
     std::vector<uint32_t> h(words * nimg);
+    // 4-element packs: the 20-word tables; 2-element: 8-word basis images (rs_chunks.hip CTabsBasis)
     for (uint32_t t = 0; t < nimg; ++t)
         for (uint32_t b = 0; b < L; ++b)
             for (uint32_t g = 0; g < (n >> (b + 1)); ++g) {
                 const uint32_t slot = n - (n >> b) + g, idx = (g << (b + 1)) + (1u << b) + t * n - 1;
-                std::copy_n(&skew_tabs[size_t(idx) * tw], tw, &h[t * words + size_t(slot) * tw]);
+                if (!e2) {
+                    std::copy_n(&skew_tabs[size_t(idx) * tw], tw, &h[t * words + size_t(slot) * tw]);
+                    continue;
+                }
+                const uint16_t lm = T.skew[idx];
+                uint32_t *dst = &h[t * words + size_t(slot) * 8];
+                auto P = [&](int i) -> uint32_t { return lm == 65535 ? 0u : T.mul(uint16_t(1u << i), lm); };
+                for (int f = 0; f < 4; ++f) {
+                    dst[2 * f] = P(2 * f) | (P(2 * f + 1) << 16);
+                    dst[2 * f + 1] = P(8 + 2 * f) | (P(9 + 2 * f) << 16);
+                }
             }
     uint32_t *d_img;
-#ifdef RS_CHUNK_REPL
-    const size_t repl_words = (h.size() + 1023) / 1024 * 1024 + 256 * 1024;  // replicas 1 MiB + apart
-    CK(hipMalloc(&d_img, repl_words * 4 * RS_CHUNK_REPL));
-    for (int r = 0; r < RS_CHUNK_REPL; ++r)
-        CK(hipMemcpy(d_img + r * repl_words, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-#else
     CK(hipMalloc(&d_img, h.size() * 4));
     CK(hipMemcpy(d_img, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-#endif
     uint8_t *orig, *rec;
     CK(hipMalloc(&orig, size_t(N) * S));
     CK(hipMalloc(&rec, size_t(M) * S));
-    CK(hipMemset(orig, 0x37, size_t(N) * S));
+    {
+        std::vector<uint8_t> hin(size_t(N) * S);
+        uint32_t x = 12345;
+        for (auto &c : hin) c = uint8_t((x = x * 1103515245u + 12345u) >> 16);
+        CK(hipMemcpy(orig, hin.data(), hin.size(), hipMemcpyHostToDevice));
+    }
     rs::MonoCore A;
     A.elems = e2 ? 2 : 4;
     A.packs = e2 ? S / 4 : S / 8;
@@ -77,9 +86,6 @@ int main(int argc, char **argv) {
     A.ifft_img_step = high ? 1 : 0;
     A.fft_img = high ? 0 : 1;
     A.fft_img_step = high ? 0 : 1;
-#ifdef RS_CHUNK_REPL
-    A.end = uint32_t(repl_words);
-#endif
     const int iters = 1000;
     const int pw = getenv("PW") ? atoi(getenv("PW")) : 1;
     auto go = [&] { CK(rs::launch_chunks(int(L), high, A, 0, pw)); };
@@ -93,8 +99,12 @@ int main(int argc, char **argv) {
     CK(hipEventSynchronize(b));
     float ms;
     CK(hipEventElapsedTime(&ms, a, b));
-    printf("k_chunks<%u, %d, %s, %d> %u:%u x %u B, %u chunks: %.2f us/launch (back-to-back)\n", L, e2 ? 2 : 4,
-           high ? "high" : "low", pw, N, M, S, C, ms * 1000 / iters);
+    std::vector<uint32_t> out(size_t(M) * S / 4);
+    CK(hipMemcpy(out.data(), rec, out.size() * 4, hipMemcpyDeviceToHost));
+    uint64_t hsh = 1469598103934665603ull;
+    for (uint32_t w : out) hsh = (hsh ^ w) * 1099511628211ull;
+    printf("k_chunks<%u, %d, %s, %d> %u:%u x %u B, %u chunks: %.2f us/launch (back-to-back), output hash %016llx\n", L,
+           e2 ? 2 : 4, high ? "high" : "low", pw, N, M, S, C, ms * 1000 / iters, (unsigned long long)hsh);
 #ifdef RS_CHUNK_STAMPS
     CK(hipDeviceSynchronize());
     go();

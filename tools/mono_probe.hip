@@ -43,13 +43,26 @@ int main(int argc, char **argv) {
     const int tw = e2 ? rs::kPerm2Words : rs::kPermWords;
     const std::vector<uint32_t> &skew_tabs = e2 ? T.perm2_by_skew : T.perm_by_skew;
     const uint32_t nimg = 65536u / n;
-    const size_t words = size_t(n - 1) * tw;
+    // 2-element packs built with RS_MONO_BASIS: 8-word basis images (rs_mono.hip Stage::kBasis)
+    const bool basis = e2 && RS_MONO_BASIS;
+    const size_t tabw = basis ? 8 : size_t(tw);
+    const size_t words = size_t(n - 1) * tabw;
     std::vector<uint32_t> h(words * nimg);
     for (uint32_t t = 0; t < nimg; ++t)
         for (uint32_t b = 0; b < L; ++b)
             for (uint32_t g = 0; g < (n >> (b + 1)); ++g) {
                 const uint32_t slot = n - (n >> b) + g, idx = (g << (b + 1)) + (1u << b) + t * n - 1;
-                std::copy_n(&skew_tabs[size_t(idx) * tw], tw, &h[t * words + size_t(slot) * tw]);
+                if (!basis) {
+                    std::copy_n(&skew_tabs[size_t(idx) * tw], tw, &h[t * words + size_t(slot) * tw]);
+                    continue;
+                }
+                const uint16_t lm = T.skew[idx];
+                auto P = [&](int i) -> uint32_t { return lm == 65535 ? 0u : T.mul(uint16_t(1u << i), lm); };
+                uint32_t *dst = &h[t * words + size_t(slot) * 8];
+                for (int f = 0; f < 4; ++f) {
+                    dst[2 * f] = P(2 * f) | (P(2 * f + 1) << 16);
+                    dst[2 * f + 1] = P(8 + 2 * f) | (P(9 + 2 * f) << 16);
+                }
             }
     uint32_t *d_img;
     CK(hipMalloc(&d_img, h.size() * 4));
