@@ -335,9 +335,9 @@ rs_status rs_check_device(rs_context *ctx);
  * turns that off again.  Multi-chunk encodes of 2^2 .. 2^7-row transforms
  * (HighRate N > pow2(M), LowRate M > pow2(N)) run as one launch whose waves
  * take the chunks in parallel (rs_chunks.hip; RS_MI355X_CHUNKS=0 at context
- * creation: never) where that measured faster: 2-element packs, HighRate or up
- * to 8 LowRate output chunks; 4-element packs, HighRate up to 8 chunks.  Adding
- * 512 sends every multi-chunk encode of those sizes there, adding 1024 none.
+ * creation: never) where that measured faster: all of them but LowRate
+ * encodes of more than 8 output chunks in 2-element packs.  Adding 512 sends
+ * every multi-chunk encode of those sizes there, adding 1024 none.
  * A/B and tests; results are identical in every mode. */
 rs_status rs_mono_enable(rs_context *ctx, int enable);
 

@@ -20,9 +20,9 @@
 // Twiddles: each wave stages its chunk's layer-ordered image (the layout of
 // k_mono's images, rs_codec.cpp mono_images: table of layer b, group g at slot
 // n - n / 2^b + g) into a wave-private LDS region of 20-word slots (16 lanes'
-// ds_read_b128 of 16 different slots then hit 16 different bank groups).  With
-// 2-element packs the images hold 8-word basis tables, expanded while staging
-// (CTabsBasis); 4-element packs stage the 20-word tables.
+// ds_read_b128 of 16 different slots then hit 16 different bank groups).  The
+// images hold 8-word basis tables (rs_codec.cpp basis_images), expanded while
+// staging (CTabsBasis, CTabsBasis4).
 //
 // Placement of a wave's n rows: lane l, register k.  Before IFFT layer b the
 // register bit holds row bit b, lane bits j < b row bits j, lane bits j >= b row
@@ -99,34 +99,6 @@ struct CRows {
     uint32_t lo[PW][2], hi[PW][2];
 };
 
-// The image pieces of one transform, issued into registers (v) and then
-// written into the wave's region (slot-padded)
-template <int L, int E>
-struct CTabs {
-    using G = ChunkGeo<L, E>;
-    uint4 v[G::KP];
-    __device__ __forceinline__ void issue(const uint32_t *img, uint32_t lane) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(img);
-        static_for<0, G::KP>([&](auto kc) {
-            const uint32_t q = lane + 64u * decltype(kc)::value;
-#ifndef RS_CHUNK_SKIP_TABS  // (tools/chunks_probe.hip ablation)
-            v[kc] = src[q < G::pieces ? q : G::pieces - 1];
-#else
-            v[kc] = uint4{q, q ^ 1u, q ^ 2u, uint32_t(reinterpret_cast<uintptr_t>(src))};
-#endif
-        });
-    }
-    __device__ __forceinline__ void write(uint32_t *region, uint32_t lane) const {
-        static_for<0, G::KP>([&](auto kc) {
-            const uint32_t q = lane + 64u * decltype(kc)::value;
-            if (q < G::pieces) {
-                const uint32_t t = q / G::PC, p = q - t * G::PC;
-                reinterpret_cast<uint4 *>(region)[t * (kSlot / 4) + p] = v[kc];
-            }
-        });
-    }
-};
-
 // 2-element tables built in the kernel from their basis images (rs_codec.cpp
 // basis_images): per table the 16 products P(e_i) = x * e_i of the multiplier with
 // the Cantor basis elements, 8 words (word 2f = P(e_2f) | P(e_2f+1) << 16 for the
@@ -168,6 +140,60 @@ struct CTabsBasis {
                 });
                 uint4 *d = reinterpret_cast<uint4 *>(region) + t * (kSlot / 4);
                 static_for<0, 4>([&](auto qc) {
+                    constexpr int q = decltype(qc)::value;
+                    d[q] = uint4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+                });
+            }
+        });
+    }
+};
+
+// 4-element tables (gf_tables.cpp fill_perm: 5 words per input byte B and output
+// byte O, 3-bit fields) from 8 basis words: per input byte B, word 4B = P0 | P1 << 16,
+// 4B + 1 = P3 | P4 << 16, 4B + 2 = P6 | P7 << 16, 4B + 3 = P2 | P5 << 16 (Pj = x * e_8B+j).
+// Field bits 0-2: entries [0, P0, P1, P0^P1] then the same XOR P2 (byte O of each);
+// bits 3-5 likewise with P3, P4, P5; bits 6-7: [0, P6, P7, P6^P7].  ~44 VALU per
+// table for 32 of its 80 bytes.
+template <int L>
+struct CTabsBasis4 {
+    static constexpr uint32_t n = 1u << L, tabs = n - 1;
+    static constexpr int KT = int((tabs + 63) / 64);
+    uint4 v[KT][2];
+    __device__ __forceinline__ void issue(const uint32_t *img, uint32_t lane) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(img);
+        static_for<0, KT>([&](auto kc) {
+            const uint32_t t = lane + 64u * decltype(kc)::value, tt = t < tabs ? t : tabs - 1;
+            v[kc][0] = src[2 * tt];
+            v[kc][1] = src[2 * tt + 1];
+        });
+    }
+    __device__ __forceinline__ void write(uint32_t *region, uint32_t lane) const {
+        static_for<0, KT>([&](auto kc) {
+            const uint32_t t = lane + 64u * decltype(kc)::value;
+            if (t < tabs) {
+                const uint32_t X[8] = {v[kc][0].x, v[kc][0].y, v[kc][0].z, v[kc][0].w,
+                                       v[kc][1].x, v[kc][1].y, v[kc][1].z, v[kc][1].w};
+                uint32_t w[20];
+                static_for<0, 2>([&](auto bc) {
+                    constexpr int B = decltype(bc)::value;
+                    const uint32_t X01 = X[4 * B], X34 = X[4 * B + 1], X67 = X[4 * B + 2], Y = X[4 * B + 3];
+                    const uint32_t t01 = X01 ^ __builtin_amdgcn_alignbit(X01, X01, 16);
+                    const uint32_t t34 = X34 ^ __builtin_amdgcn_alignbit(X34, X34, 16);
+                    const uint32_t t67 = X67 ^ __builtin_amdgcn_alignbit(X67, X67, 16);
+                    static_for<0, 2>([&](auto oc) {
+                        constexpr int O = decltype(oc)::value;
+                        constexpr uint32_t sel = O ? 0x0503010Cu : 0x0402000Cu;
+                        constexpr uint32_t r2 = O ? 0x01010101u : 0x00000000u, r5 = O ? 0x03030303u : 0x02020202u;
+                        uint32_t *o = w + (2 * B + O) * 5;
+                        o[0] = __builtin_amdgcn_perm(t01, X01, sel);
+                        o[1] = o[0] ^ __builtin_amdgcn_perm(Y, Y, r2);
+                        o[2] = __builtin_amdgcn_perm(t34, X34, sel);
+                        o[3] = o[2] ^ __builtin_amdgcn_perm(Y, Y, r5);
+                        o[4] = __builtin_amdgcn_perm(t67, X67, sel);
+                    });
+                });
+                uint4 *d = reinterpret_cast<uint4 *>(region) + t * (kSlot / 4);
+                static_for<0, 5>([&](auto qc) {
                     constexpr int q = decltype(qc)::value;
                     d[q] = uint4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
                 });
@@ -331,7 +357,7 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_chunks(const MonoCore A) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t W = blockDim.x >> 6;
     uint32_t *region = lds + wave * G::region;
-    std::conditional_t<E == 2, CTabsBasis<L>, CTabs<L, E>> tabs;  // (E = 2: basis images)
+    std::conditional_t<E == 2, CTabsBasis<L>, CTabsBasis4<L>> tabs;  // basis images, both formats
     RS_CSTAMP(0);
     const uint32_t *img_base = A.img;
     if constexpr (HIGH) {

@@ -230,6 +230,7 @@ struct rs_context {
     uint32_t *d_img[13] = {};     // column-kernel twiddle images per L (built at context creation)
     uint32_t *d_img2[13] = {};    // the same in the 2-element table format
     uint32_t *d_imgb[13] = {};    // 8-word basis images of the 2-element format (basis_images)
+    uint32_t *d_imgb4[8] = {};    // the same for the 4-element format, 2^2..2^7 rows
     std::mutex host_engine_mu;  // guards host_engine_buf (rs_engine_*_host staging)
     DevBuf host_engine_buf;
     std::mutex mu;  // guards ws_by_stream (device-resident API scratch), prof, recs
@@ -526,10 +527,12 @@ const uint32_t *mono_images(rs_context *ctx, uint32_t L, uint32_t elems = 4) {
 // products P(e_i) = x * e_i of the table's multiplier with the 16 Cantor basis
 // elements, word 2f = P(e_2f) | P(e_2f+1) << 16 (the low byte's 2-bit field f),
 // word 2f + 1 = P(e_8+2f) | P(e_9+2f) << 16 (the high byte's); zero for skew 65535.
+// 4-element format (rs_chunks.hip CTabsBasis4): per input byte B, words 4B .. 4B + 3 =
+// P0 | P1 << 16, P3 | P4 << 16, P6 | P7 << 16, P2 | P5 << 16 with Pj = P(e_8B+j).
 constexpr uint32_t kBasisWords = 8;
-const uint32_t *basis_images(rs_context *ctx, uint32_t L) {
+const uint32_t *basis_images(rs_context *ctx, uint32_t L, uint32_t elems = 2) {
     std::lock_guard<std::mutex> lock(ctx->img_mu);
-    uint32_t *&slot_ptr = ctx->d_imgb[L];
+    uint32_t *&slot_ptr = elems == 2 ? ctx->d_imgb[L] : ctx->d_imgb4[L];
     if (slot_ptr) return slot_ptr;
     const rs::GfTables &T = rs::tables();
     const uint32_t n = 1u << L, nimg = 65536u / n;
@@ -543,9 +546,20 @@ const uint32_t *basis_images(rs_context *ctx, uint32_t L) {
                 const uint32_t idx = (g << (b + 1)) + (1u << b) + t * n - 1;
                 const uint16_t lm = T.skew[idx];
                 auto P = [&](int i) -> uint32_t { return lm == 65535 ? 0u : T.mul(uint16_t(1u << i), lm); };
-                for (uint32_t f = 0; f < 4; ++f) {
-                    dst[size_t(slot) * kBasisWords + 2 * f] = P(int(2 * f)) | (P(int(2 * f + 1)) << 16);
-                    dst[size_t(slot) * kBasisWords + 2 * f + 1] = P(int(8 + 2 * f)) | (P(int(9 + 2 * f)) << 16);
+                uint32_t *o = dst + size_t(slot) * kBasisWords;
+                if (elems == 2) {
+                    for (uint32_t f = 0; f < 4; ++f) {
+                        o[2 * f] = P(int(2 * f)) | (P(int(2 * f + 1)) << 16);
+                        o[2 * f + 1] = P(int(8 + 2 * f)) | (P(int(9 + 2 * f)) << 16);
+                    }
+                } else {
+                    for (int B = 0; B < 2; ++B) {
+                        const int j = 8 * B;
+                        o[4 * B] = P(j) | (P(j + 1) << 16);
+                        o[4 * B + 1] = P(j + 3) | (P(j + 4) << 16);
+                        o[4 * B + 2] = P(j + 6) | (P(j + 7) << 16);
+                        o[4 * B + 3] = P(j + 2) | (P(j + 5) << 16);
+                    }
                 }
             }
     }
@@ -615,29 +629,30 @@ bool try_lane(rs_context *ctx, uint32_t L, uint32_t chunks, const rs::MonoArgs &
 
 // Multi-chunk encodes of small transforms (rs_chunks.hip): one launch in which the
 // waves of a pack's workgroup take the chunks in parallel (HighRate input chunks,
-// LowRate output chunks).  One stripe; the column kernel's pack bound.  Routed by
-// default where it measured faster than the passes (profiles/r05h/chunks_*.jsonl,
-// wall us per call at 1 KiB shards): with 2-element packs (basis tables) every
-// HighRate shape (1000:100 13.2 -> 6.5, 9000:100 35.2 -> 21.1, 100:10 7.9 -> 4.9) and
-// LowRate up to 8 output chunks (128:1024 8.2 -> 6.2; 64:640 and 100:9000, one pass
-// with the chunks over the grid, tie or win); with 4-element packs (20-word tables)
-// HighRate up to 8 chunks (1000:100 x 2 KiB 13.1 -> 12.3; LowRate 128:1024 x 2 KiB
-// 8.5 -> 11.4 stays on the pass).  rs_mono_enable + 512 / RS_MI355X_CHUNKS=2: every shape.
+// LowRate output chunks), twiddle tables built in LDS from basis images.  One
+// stripe; the column kernel's pack bound.  Measured against the passes (wall us
+// per call, profiles/r05h/chunks{,4}_{forced,none}.jsonl): 1000:100 x 1 KiB 13.2 ->
+// 6.5, x 2 KiB 13.5 -> 7.8; 9000:100 x 1 / 2 KiB 35.2 / 57.0 -> 21.1 / 24.7; 100:10
+// 7.9 -> 4.9; LowRate 128:1024 x 1 / 2 KiB 8.2 / 8.6 -> 6.2 / 7.3.  The exception,
+// LowRate with 2-element packs past 8 output chunks (64:640 5.86 / 5.87, 100:9000
+// x 1 KiB 21.7 -> 22.6), stays on the pass.  rs_mono_enable + 512 / RS_MI355X_CHUNKS=2:
+// every supported shape.
 bool use_chunks(rs_context *ctx, uint32_t L, const Geom &g, uint32_t chunks, bool high) {
     // (RS_MI355X_CHUNK_PARALLEL forces one of the pass forms: tests, A/B)
+    // (HighRate up to twice the pack bound, two packs per wave: 1000:100 x 4 KiB 13.7 -> 9.3 us,
+    // profiles/r05h/chunks4_pw.txt; LowRate there lost, 8.8 -> 10.2)
     if (!ctx->chunks || !ctx->mono || ctx->mono_all || ctx->chunk_par >= 0 || chunks < 2 || g.stripes != 1 ||
-        !rs::chunks_supported(int(L)) || g.packs > ctx->mono_max_packs)
+        !rs::chunks_supported(int(L)) || g.packs > (high ? 2 : 1) * ctx->mono_max_packs)
         return false;
     const bool e2 = ctx->e2_encode && uint64_t(g.packs) <= ctx->e2_max_packs;  // as mono_args decides
-    return ctx->chunks_forced || (e2 ? high || chunks <= kChunksMaxWaves : high && chunks <= kChunksMaxWaves);
+    return ctx->chunks_forced || high || !e2 || chunks <= kChunksMaxWaves;
 }
 void launch_chunks(rs_context *ctx, const Geom &g, bool high, uint32_t L, const rs::RowMap &src, const rs::RowMap &dst,
                    uint32_t chunks, uint64_t bytes, hipStream_t s) {
     rs::MonoArgs Mo = mono_args(ctx, L, g, true);
-    if (Mo.elems == 2) {  // 2-element packs: basis images, expanded in the kernel (rs_chunks.hip CTabsBasis)
-        Mo.img = basis_images(ctx, L);
-        Mo.img_words = uint64_t((1u << L) - 1) * kBasisWords;
-    }
+    // basis images, expanded in the kernel (rs_chunks.hip CTabsBasis / CTabsBasis4)
+    Mo.img = basis_images(ctx, L, Mo.elems);
+    Mo.img_words = uint64_t((1u << L) - 1) * kBasisWords;
     Mo.src[0] = src;
     Mo.nsrc = 1;
     Mo.dst = dst;
@@ -646,9 +661,10 @@ void launch_chunks(rs_context *ctx, const Geom &g, bool high, uint32_t L, const 
     Mo.ifft_img_step = high ? 1 : 0;
     Mo.fft_img = high ? 0 : 1;  // LowRate output chunk c: skew offset c n + n
     Mo.fft_img_step = high ? 0 : 1;
+    const int pw = g.packs > ctx->mono_max_packs ? 2 : 1;  // packs per wave (use_chunks' wide shapes)
     hipEvent_t ev = nullptr;
     if (t_prof_ctx) prof_begin(s, &ev);
-    check(rs::launch_chunks(int(L), high, Mo, s));
+    check(rs::launch_chunks(int(L), high, Mo, s, pw));
     if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), bytes);
 }
 
@@ -1537,6 +1553,7 @@ rs_status rs_context_create(int device, rs_context **out) {
         for (uint32_t L = kChunksMinL; L <= kMonoMaxL; ++L) mono_images(ctx, L);
         for (uint32_t L = kChunksMinL; L <= 11; ++L) mono_images(ctx, L, 2);
         for (uint32_t L = kChunksMinL; L <= (RS_MONO_BASIS ? 11u : 7u); ++L) basis_images(ctx, L);
+        for (uint32_t L = kChunksMinL; L <= 7; ++L) basis_images(ctx, L, 4);
         return RS_OK;
     });
     if (st != RS_OK) {
@@ -1559,6 +1576,8 @@ void rs_context_destroy(rs_context *ctx) {
     for (uint32_t *p : ctx->d_img2)
         if (p) (void)hipFree(p);
     for (uint32_t *p : ctx->d_imgb)
+        if (p) (void)hipFree(p);
+    for (uint32_t *p : ctx->d_imgb4)
         if (p) (void)hipFree(p);
     if (ctx->d_lwfold_base) (void)hipFree(ctx->d_lwfold_base);
     for (uint32_t *p : ctx->d_img)

@@ -966,6 +966,8 @@ CHUNKS_CASES = [
     ("high", 300, 30, 64), ("high", 100, 10, 6), ("high", 50, 5, 64), ("high", 20, 3, 2), ("high", 9000, 100, 2),
     ("low", 128, 1024, 1024), ("low", 100, 1000, 256), ("low", 64, 640, 130), ("low", 10, 100, 64),
     ("low", 3, 20, 6), ("low", 100, 9000, 2), ("default", 4000, 120, 64), ("default", 5, 41, 320),
+    # two packs per wave past 256 4-element packs (HighRate), odd pack counts, tails
+    ("high", 1000, 100, 4096), ("high", 600, 100, 3000), ("high", 300, 60, 2050),
 ]
 
 

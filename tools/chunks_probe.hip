@@ -41,23 +41,29 @@ int main(int argc, char **argv) {
     const int tw = e2 ? rs::kPerm2Words : rs::kPermWords;
     const std::vector<uint32_t> &skew_tabs = e2 ? T.perm2_by_skew : T.perm_by_skew;
     const uint32_t nimg = 65536u / n;
-    const size_t words = size_t(n - 1) * (e2 ? 8 : tw);
+    const size_t words = size_t(n - 1) * 8;
     std::vector<uint32_t> h(words * nimg);
     // 4-element packs: the 20-word tables; 2-element: 8-word basis images (rs_chunks.hip CTabsBasis)
     for (uint32_t t = 0; t < nimg; ++t)
         for (uint32_t b = 0; b < L; ++b)
             for (uint32_t g = 0; g < (n >> (b + 1)); ++g) {
                 const uint32_t slot = n - (n >> b) + g, idx = (g << (b + 1)) + (1u << b) + t * n - 1;
-                if (!e2) {
-                    std::copy_n(&skew_tabs[size_t(idx) * tw], tw, &h[t * words + size_t(slot) * tw]);
-                    continue;
-                }
                 const uint16_t lm = T.skew[idx];
                 uint32_t *dst = &h[t * words + size_t(slot) * 8];
                 auto P = [&](int i) -> uint32_t { return lm == 65535 ? 0u : T.mul(uint16_t(1u << i), lm); };
-                for (int f = 0; f < 4; ++f) {
-                    dst[2 * f] = P(2 * f) | (P(2 * f + 1) << 16);
-                    dst[2 * f + 1] = P(8 + 2 * f) | (P(9 + 2 * f) << 16);
+                if (e2) {
+                    for (int f = 0; f < 4; ++f) {
+                        dst[2 * f] = P(2 * f) | (P(2 * f + 1) << 16);
+                        dst[2 * f + 1] = P(8 + 2 * f) | (P(9 + 2 * f) << 16);
+                    }
+                } else {
+                    for (int B = 0; B < 2; ++B) {
+                        const int j = 8 * B;
+                        dst[4 * B] = P(j) | (P(j + 1) << 16);
+                        dst[4 * B + 1] = P(j + 3) | (P(j + 4) << 16);
+                        dst[4 * B + 2] = P(j + 6) | (P(j + 7) << 16);
+                        dst[4 * B + 3] = P(j + 2) | (P(j + 5) << 16);
+                    }
                 }
             }
     uint32_t *d_img;
