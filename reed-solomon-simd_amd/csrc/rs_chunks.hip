@@ -171,32 +171,10 @@ struct CTabsBasis4 {
         static_for<0, KT>([&](auto kc) {
             const uint32_t t = lane + 64u * decltype(kc)::value;
             if (t < tabs) {
-                const uint32_t X[8] = {v[kc][0].x, v[kc][0].y, v[kc][0].z, v[kc][0].w,
-                                       v[kc][1].x, v[kc][1].y, v[kc][1].z, v[kc][1].w};
-                uint32_t w[20];
-                static_for<0, 2>([&](auto bc) {
-                    constexpr int B = decltype(bc)::value;
-                    const uint32_t X01 = X[4 * B], X34 = X[4 * B + 1], X67 = X[4 * B + 2], Y = X[4 * B + 3];
-                    const uint32_t t01 = X01 ^ __builtin_amdgcn_alignbit(X01, X01, 16);
-                    const uint32_t t34 = X34 ^ __builtin_amdgcn_alignbit(X34, X34, 16);
-                    const uint32_t t67 = X67 ^ __builtin_amdgcn_alignbit(X67, X67, 16);
-                    static_for<0, 2>([&](auto oc) {
-                        constexpr int O = decltype(oc)::value;
-                        constexpr uint32_t sel = O ? 0x0503010Cu : 0x0402000Cu;
-                        constexpr uint32_t r2 = O ? 0x01010101u : 0x00000000u, r5 = O ? 0x03030303u : 0x02020202u;
-                        uint32_t *o = w + (2 * B + O) * 5;
-                        o[0] = __builtin_amdgcn_perm(t01, X01, sel);
-                        o[1] = o[0] ^ __builtin_amdgcn_perm(Y, Y, r2);
-                        o[2] = __builtin_amdgcn_perm(t34, X34, sel);
-                        o[3] = o[2] ^ __builtin_amdgcn_perm(Y, Y, r5);
-                        o[4] = __builtin_amdgcn_perm(t67, X67, sel);
-                    });
-                });
+                uint4 o[5];
+                basis4_expand(v[kc][0], v[kc][1], o);
                 uint4 *d = reinterpret_cast<uint4 *>(region) + t * (kSlot / 4);
-                static_for<0, 5>([&](auto qc) {
-                    constexpr int q = decltype(qc)::value;
-                    d[q] = uint4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
-                });
+                static_for<0, 5>([&](auto qc) { d[decltype(qc)::value] = o[decltype(qc)::value]; });
             }
         });
     }

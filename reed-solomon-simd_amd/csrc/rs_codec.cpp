@@ -226,6 +226,12 @@ struct rs_context {
     bool pad_small = true;        // decodes of 16..64 work rows on the 2^7-row column kernel (RS_MI355X_PAD_SMALL)
     int chunk_par = -1;           // RS_MI355X_CHUNK_PARALLEL: -1 by pack count (chunk_parallel), 0 / 1 forced
     uint32_t *d_lut2 = nullptr;   // perm2_by_log: the 2-element form of d_lut
+    // the pass kernels' tables as 8-word bases (rs_kernels.hip BasisStager; RS_MI355X_PASS_BASIS=1).
+    // Off by default: within +-2.5 % of the 20-word tables on 9 pass shapes, slower on the small
+    // ones (4096:4096 x 1 KiB decode 100 % 39.4 -> 40.3 us, 8192:8192 x 64 KiB encode 1028 ->
+    // 1003 us; profiles/r05h/passbasis_*.jsonl)
+    uint32_t *d_twb = nullptr, *d_lutb = nullptr;  // by skew index / by log factor
+    bool pass_basis = false;
     std::mutex img_mu;            // guards d_img, d_img2
     uint32_t *d_img[13] = {};     // column-kernel twiddle images per L (built at context creation)
     uint32_t *d_img2[13] = {};    // the same in the 2-element table format
@@ -413,8 +419,9 @@ rs::PassArgs base_args(rs_context *ctx, const Geom &g, uint32_t n) {
     A.n = n;
     A.packs = g.packs;
     A.slices = (g.packs + 63) / 64;
-    A.tw = ctx->d_tw;
-    A.lut = ctx->d_lut;
+    A.tw = ctx->pass_basis ? ctx->d_twb : ctx->d_tw;
+    A.lut = ctx->pass_basis ? ctx->d_lutb : ctx->d_lut;
+    A.tab_basis = ctx->pass_basis ? 1u : 0u;
     A.fmt = g.fmt;
     return A;
 }
@@ -530,6 +537,20 @@ const uint32_t *mono_images(rs_context *ctx, uint32_t L, uint32_t elems = 4) {
 // 4-element format (rs_chunks.hip CTabsBasis4): per input byte B, words 4B .. 4B + 3 =
 // P0 | P1 << 16, P3 | P4 << 16, P6 | P7 << 16, P2 | P5 << 16 with Pj = P(e_8B+j).
 constexpr uint32_t kBasisWords = 8;
+// The 4-element basis of multiplier log lm (rs_gf.hpp basis4_expand's layout); zero
+// when !nonzero or lm = 65535 as a skew (multiply by zero)
+void basis4_words(const rs::GfTables &T, uint32_t lm, bool nonzero, uint32_t *o) {
+    auto P = [&](int i) -> uint32_t {
+        return !nonzero || lm > 65535u ? 0u : T.mul(uint16_t(1u << i), uint16_t(lm));
+    };
+    for (int B = 0; B < 2; ++B) {
+        const int j = 8 * B;
+        o[4 * B] = P(j) | (P(j + 1) << 16);
+        o[4 * B + 1] = P(j + 3) | (P(j + 4) << 16);
+        o[4 * B + 2] = P(j + 6) | (P(j + 7) << 16);
+        o[4 * B + 3] = P(j + 2) | (P(j + 5) << 16);
+    }
+}
 const uint32_t *basis_images(rs_context *ctx, uint32_t L, uint32_t elems = 2) {
     std::lock_guard<std::mutex> lock(ctx->img_mu);
     uint32_t *&slot_ptr = elems == 2 ? ctx->d_imgb[L] : ctx->d_imgb4[L];
@@ -1507,6 +1528,18 @@ rs_status rs_context_create(int device, rs_context **out) {
         check(hipMalloc(&ctx->d_lut2, T.perm2_by_log.size() * 4));
         check(hipMemcpy(ctx->d_lut2, T.perm2_by_log.data(), T.perm2_by_log.size() * 4, hipMemcpyHostToDevice));
         ctx->lw0 = T.log_walsh[0];
+        if (const char *pb = getenv("RS_MI355X_PASS_BASIS")) ctx->pass_basis = pb[0] == '1';
+        {  // 4-element basis tables by skew index (zero for skew 65535) and by log factor
+            std::vector<uint32_t> tw(size_t(65536) * kBasisWords), lu(size_t(65536) * kBasisWords);
+            for (uint32_t i = 0; i < 65536; ++i) {
+                basis4_words(T, i < 65535 ? T.skew[i] : 65535u, i < 65535 && T.skew[i] != 65535, &tw[size_t(i) * kBasisWords]);
+                basis4_words(T, uint16_t(i), true, &lu[size_t(i) * kBasisWords]);
+            }
+            check(hipMalloc(&ctx->d_twb, tw.size() * 4));
+            check(hipMalloc(&ctx->d_lutb, lu.size() * 4));
+            check(hipMemcpy(ctx->d_twb, tw.data(), tw.size() * 4, hipMemcpyHostToDevice));
+            check(hipMemcpy(ctx->d_lutb, lu.data(), lu.size() * 4, hipMemcpyHostToDevice));
+        }
         int cus = 0;
         check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         ctx->e2_max_packs = ctx->e2_default = cus > 1 ? uint32_t(cus) / 2 : 1u;
@@ -1572,6 +1605,8 @@ void rs_context_destroy(rs_context *ctx) {
     if (ctx->d_tw) (void)hipFree(ctx->d_tw);
     if (ctx->d_lut) (void)hipFree(ctx->d_lut);
     if (ctx->d_lut2) (void)hipFree(ctx->d_lut2);
+    if (ctx->d_twb) (void)hipFree(ctx->d_twb);
+    if (ctx->d_lutb) (void)hipFree(ctx->d_lutb);
     if (ctx->d_top) (void)hipFree(ctx->d_top);
     for (uint32_t *p : ctx->d_img2)
         if (p) (void)hipFree(p);

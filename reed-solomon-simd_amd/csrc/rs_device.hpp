@@ -140,6 +140,8 @@ struct PassArgs {
 
     const uint32_t *tw = nullptr;       // perm tables indexed by skew index (zero table = no multiply)
     const uint32_t *lut = nullptr;      // perm tables indexed by log factor
+    // tw / lut hold 8-word basis tables (rs_codec.cpp basis tables), expanded while staging
+    uint32_t tab_basis = 0;
     ShardFormat fmt;                    // byte layout of src / dst (work buffers: whole blocks)
 
     // ---- 2-level decodes (blk_masks = 1): per block b = row >> blk_shift (b < 256),

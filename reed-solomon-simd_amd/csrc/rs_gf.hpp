@@ -82,6 +82,38 @@ __device__ __forceinline__ void gf_muladd4(uint32_t &acc_l, uint32_t &acc_h, uin
     acc_h = xor3(acc_h, ha, hb);
 }
 
+// The 20-word table of a multiplier from its 8-word basis (rs_codec.cpp
+// basis_images / basis tables): multiplication by a constant is GF(2)-linear, so
+// a 3-bit field's 8 lookups are [0, p0, p1, p0^p1] and that word XOR p2
+// (byte O of the products pj = x * e_8B+j of input byte B).  Basis words, per
+// input byte B: 4B = P0 | P1 << 16, 4B + 1 = P3 | P4 << 16, 4B + 2 = P6 | P7 << 16,
+// 4B + 3 = P2 | P5 << 16.  Output: table pieces o[0..4] (words 4q .. 4q + 3 of
+// fill_perm's layout, gf_tables.cpp).  ~44 VALU for 32 of the table's 80 bytes.
+__device__ __forceinline__ void basis4_expand(const uint4 &b0, const uint4 &b1, uint4 (&o)[5]) {
+    const uint32_t X[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    uint32_t w[20];
+#pragma unroll
+    for (int B = 0; B < 2; ++B) {
+        const uint32_t X01 = X[4 * B], X34 = X[4 * B + 1], X67 = X[4 * B + 2], Y = X[4 * B + 3];
+        const uint32_t t01 = X01 ^ __builtin_amdgcn_alignbit(X01, X01, 16);
+        const uint32_t t34 = X34 ^ __builtin_amdgcn_alignbit(X34, X34, 16);
+        const uint32_t t67 = X67 ^ __builtin_amdgcn_alignbit(X67, X67, 16);
+#pragma unroll
+        for (int O = 0; O < 2; ++O) {
+            const uint32_t sel = O ? 0x0503010Cu : 0x0402000Cu;
+            const uint32_t r2 = O ? 0x01010101u : 0x00000000u, r5 = O ? 0x03030303u : 0x02020202u;
+            uint32_t *t = w + (2 * B + O) * 5;
+            t[0] = __builtin_amdgcn_perm(t01, X01, sel);
+            t[1] = t[0] ^ __builtin_amdgcn_perm(Y, Y, r2);
+            t[2] = __builtin_amdgcn_perm(t34, X34, sel);
+            t[3] = t[2] ^ __builtin_amdgcn_perm(Y, Y, r5);
+            t[4] = __builtin_amdgcn_perm(t67, X67, sel);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 5; ++q) o[q] = uint4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+}
+
 __device__ __forceinline__ void gf_mul4(uint32_t &xl, uint32_t &xh, const uint32_t *__restrict__ t) {
     uint32_t l = 0, h = 0;
     gf_muladd4(l, h, xl, xh, t);

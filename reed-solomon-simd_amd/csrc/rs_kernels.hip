@@ -140,6 +140,97 @@ __device__ __forceinline__ uint4 twiddle_piece(const PassArgs &A, const Ctx &c, 
 // load() issues every global load into registers, store() writes LDS.  NT =
 // workgroup size.  Twiddles: one round trip; decode row tables: two (their
 // address depends on the row's log factor).  No barrier.
+// Basis tables (PassArgs::tab_basis): 2 pieces per table instead of 5, one table
+// per thread, built into its 5 LDS pieces by basis4_expand (rs_gf.hpp).
+template <int K>
+__device__ __forceinline__ uint32_t twiddle_index(const Ctx &c, uint32_t delta, uint32_t slot) {
+    const uint32_t y = (1u << K) - slot;            // in [2, 2^K]
+    const int b = K - (32 - __builtin_clz(y - 1));  // K - ceil(log2 y)
+    const uint32_t grp = slot - ((1u << K) - (1u << (K - b)));
+    const uint32_t row = c.grow(grp << (b + 1), K);
+    const uint32_t gb = c.a + b;
+    return (row & ~((2u << gb) - 1u)) + (1u << gb) + delta - 1u;
+}
+template <int K, int NT>
+struct BasisStager {
+    static constexpr uint32_t kTw = (1u << K) - 1, kRw = 1u << K;  // tables
+    static constexpr int PT = kTw ? (kTw + NT - 1) / NT : 1, PR = (kRw + NT - 1) / NT;
+    uint4 vi[PT][2], vf[PT][2], vs[PR][2], vv[PR][2];
+    uint32_t ri = 0;
+    template <typename ST>
+    __device__ __forceinline__ void load(const ST &st, const PassArgs &A, const Ctx &c, uint32_t chunk) {
+        const uint32_t tid = threadIdx.x;
+        const uint32_t dI = A.ifft_delta + chunk * A.ifft_delta_step, dF = A.fft_delta + chunk * A.fft_delta_step;
+        const uint4 *tw = reinterpret_cast<const uint4 *>(A.tw);
+        if (st.tabI || st.tabF) {
+#pragma unroll
+            for (int k = 0; k < PT; ++k) {
+                const uint32_t t = tid + uint32_t(k) * NT;
+                if (t < kTw) {
+                    if (st.tabI) {
+                        const uint32_t i = twiddle_index<K>(c, dI, t);
+                        vi[k][0] = tw[2 * i], vi[k][1] = tw[2 * i + 1];
+                    }
+                    if (st.tabF) {
+                        const uint32_t i = twiddle_index<K>(c, dF, t);
+                        vf[k][0] = tw[2 * i], vf[k][1] = tw[2 * i + 1];
+                    }
+                }
+            }
+        }
+        if (st.tabS || st.tabV) {
+            uint32_t f[PR];
+#pragma unroll
+            for (int k = 0; k < PR; ++k) {
+                const uint32_t t = tid + uint32_t(k) * NT;
+                if (t < kRw) f[k] = st.ri_lds ? st.ri_lds[t] : A.rowinfo[c.grow(t, K) + chunk * A.n];
+            }
+            if (tid < (1u << K) && !st.ri_lds) ri = A.rowinfo[c.grow(tid, K) + chunk * A.n];
+            const uint4 *lut = reinterpret_cast<const uint4 *>(A.lut);
+#pragma unroll
+            for (int k = 0; k < PR; ++k) {
+                const uint32_t t = tid + uint32_t(k) * NT;
+                if (t < kRw) {
+                    const uint32_t lf = f[k] & 0xFFFFu;
+                    if (st.tabS) vs[k][0] = lut[2 * lf], vs[k][1] = lut[2 * lf + 1];
+                    if (st.tabV) vv[k][0] = lut[2 * (65535u - lf)], vv[k][1] = lut[2 * (65535u - lf) + 1];
+                }
+            }
+        }
+    }
+    template <typename ST>
+    __device__ __forceinline__ void store(const ST &st) const {
+        const uint32_t tid = threadIdx.x;
+        auto put = [](uint32_t *tab, uint32_t t, const uint4 (&v)[2]) {
+            uint4 o[5];
+            basis4_expand(v[0], v[1], o);
+#pragma unroll
+            for (int q = 0; q < 5; ++q) reinterpret_cast<uint4 *>(tab)[t * 5 + q] = o[q];
+        };
+        if (st.tabI || st.tabF) {
+#pragma unroll
+            for (int k = 0; k < PT; ++k) {
+                const uint32_t t = tid + uint32_t(k) * NT;
+                if (t < kTw) {
+                    if (st.tabI) put(st.tabI, t, vi[k]);
+                    if (st.tabF) put(st.tabF, t, vf[k]);
+                }
+            }
+        }
+        if (st.tabS || st.tabV) {
+            if (tid < (1u << K) && !st.ri_lds) st.rinfo[tid] = ri;
+#pragma unroll
+            for (int k = 0; k < PR; ++k) {
+                const uint32_t t = tid + uint32_t(k) * NT;
+                if (t < kRw) {
+                    if (st.tabS) put(st.tabS, t, vs[k]);
+                    if (st.tabV) put(st.tabV, t, vv[k]);
+                }
+            }
+        }
+    }
+};
+
 template <int K, int NT>
 struct Stager {
     // in 16-byte pieces: 5 per 20-word table
@@ -149,11 +240,18 @@ struct Stager {
     const uint32_t *ri_lds = nullptr;  // row info already in LDS (fused eval_poly: one set, chunk 0)
     uint4 vi[PT], vf[PT], vs[PR], vv[PR];
     uint32_t ri = 0;
+    BasisStager<K, NT> bs;
+    bool basis = false;
 
     __device__ __forceinline__ void load(const PassArgs &A, const Ctx &c, uint32_t chunk) {
 #ifdef RS_PROBE_SKIP_STAGE  // tools/pass_probe.hip: time a pass without table staging
         return;
 #endif
+        basis = A.tab_basis != 0;
+        if (basis) {
+            bs.load(*this, A, c, chunk);
+            return;
+        }
         const uint32_t tid = threadIdx.x;
         const uint32_t dI = A.ifft_delta + chunk * A.ifft_delta_step, dF = A.fft_delta + chunk * A.fft_delta_step;
         if (tabI || tabF) {
@@ -191,6 +289,10 @@ struct Stager {
 #ifdef RS_PROBE_SKIP_STAGE
         return;
 #endif
+        if (basis) {
+            bs.store(*this);
+            return;
+        }
         const uint32_t tid = threadIdx.x;
         if (tabI || tabF) {
 #pragma unroll
