@@ -551,6 +551,24 @@ void basis4_words(const rs::GfTables &T, uint32_t lm, bool nonzero, uint32_t *o)
         o[4 * B + 3] = P(j + 2) | (P(j + 5) << 16);
     }
 }
+// The pass kernels' basis tables (PassArgs::tab_basis): 4-element bases by skew
+// index (zero for skew 65535) and by log factor; built when first needed.
+void pass_basis_tables(rs_context *ctx) {
+    std::lock_guard<std::mutex> lock(ctx->img_mu);
+    if (ctx->d_twb) return;
+    const rs::GfTables &T = rs::tables();
+    std::vector<uint32_t> tw(size_t(65536) * kBasisWords), lu(size_t(65536) * kBasisWords);
+    for (uint32_t i = 0; i < 65536; ++i) {
+        basis4_words(T, i < 65535 ? T.skew[i] : 65535u, i < 65535 && T.skew[i] != 65535, &tw[size_t(i) * kBasisWords]);
+        basis4_words(T, uint16_t(i), true, &lu[size_t(i) * kBasisWords]);
+    }
+    check(hipMalloc(&ctx->d_lutb, lu.size() * 4));
+    check(hipMemcpy(ctx->d_lutb, lu.data(), lu.size() * 4, hipMemcpyHostToDevice));
+    uint32_t *d = nullptr;
+    check(hipMalloc(&d, tw.size() * 4));
+    check(hipMemcpy(d, tw.data(), tw.size() * 4, hipMemcpyHostToDevice));
+    ctx->d_twb = d;
+}
 const uint32_t *basis_images(rs_context *ctx, uint32_t L, uint32_t elems = 2) {
     std::lock_guard<std::mutex> lock(ctx->img_mu);
     uint32_t *&slot_ptr = elems == 2 ? ctx->d_imgb[L] : ctx->d_imgb4[L];
@@ -1529,17 +1547,7 @@ rs_status rs_context_create(int device, rs_context **out) {
         check(hipMemcpy(ctx->d_lut2, T.perm2_by_log.data(), T.perm2_by_log.size() * 4, hipMemcpyHostToDevice));
         ctx->lw0 = T.log_walsh[0];
         if (const char *pb = getenv("RS_MI355X_PASS_BASIS")) ctx->pass_basis = pb[0] == '1';
-        {  // 4-element basis tables by skew index (zero for skew 65535) and by log factor
-            std::vector<uint32_t> tw(size_t(65536) * kBasisWords), lu(size_t(65536) * kBasisWords);
-            for (uint32_t i = 0; i < 65536; ++i) {
-                basis4_words(T, i < 65535 ? T.skew[i] : 65535u, i < 65535 && T.skew[i] != 65535, &tw[size_t(i) * kBasisWords]);
-                basis4_words(T, uint16_t(i), true, &lu[size_t(i) * kBasisWords]);
-            }
-            check(hipMalloc(&ctx->d_twb, tw.size() * 4));
-            check(hipMalloc(&ctx->d_lutb, lu.size() * 4));
-            check(hipMemcpy(ctx->d_twb, tw.data(), tw.size() * 4, hipMemcpyHostToDevice));
-            check(hipMemcpy(ctx->d_lutb, lu.data(), lu.size() * 4, hipMemcpyHostToDevice));
-        }
+        if (ctx->pass_basis) pass_basis_tables(ctx);
         int cus = 0;
         check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         ctx->e2_max_packs = ctx->e2_default = cus > 1 ? uint32_t(cus) / 2 : 1u;
