@@ -656,9 +656,9 @@ void launch_mono(int mode, uint32_t L, const rs::MonoArgs &M, hipStream_t s, uin
 bool try_lane(rs_context *ctx, uint32_t L, uint32_t chunks, const rs::MonoArgs &M, hipStream_t s, uint64_t bytes) {
     if (!ctx->lane || chunks != 1 || M.elems != 2 || int(L) > ctx->lane_max_l || !rs::lane_supported(int(L)))
         return false;
-    rs::MonoArgs F = M;  // the lane kernel stages the 16-word tables
-    F.img = mono_images(ctx, L, 2);
-    F.img_words = uint64_t((1u << L) - 1) * rs::kPerm2Words;
+    rs::MonoArgs F = M;  // the lane kernel stages basis or 16-word images (RS_LANE_BASIS)
+    F.img = RS_LANE_BASIS ? basis_images(ctx, L, 2) : mono_images(ctx, L, 2);
+    F.img_words = uint64_t((1u << L) - 1) * (RS_LANE_BASIS ? kBasisWords : rs::kPerm2Words);
     hipEvent_t ev = nullptr;
     if (t_prof_ctx) prof_begin(s, &ev);
     check(rs::launch_lane(int(L), F, s));
@@ -1593,7 +1593,7 @@ rs_status rs_context_create(int device, rs_context **out) {
         // synchronous upload the first time a size is seen
         for (uint32_t L = kChunksMinL; L <= kMonoMaxL; ++L) mono_images(ctx, L);
         for (uint32_t L = kChunksMinL; L <= 11; ++L) mono_images(ctx, L, 2);
-        for (uint32_t L = kChunksMinL; L <= (RS_MONO_BASIS ? 11u : 7u); ++L) basis_images(ctx, L);
+        for (uint32_t L = kChunksMinL; L <= (RS_MONO_BASIS ? 11u : 10u); ++L) basis_images(ctx, L);  // (k_lane: 8..10)
         for (uint32_t L = kChunksMinL; L <= 7; ++L) basis_images(ctx, L, 4);
         return RS_OK;
     });

@@ -197,6 +197,12 @@ char *launch_name_buf();
 #ifndef RS_MONO_BASIS
 #define RS_MONO_BASIS 0
 #endif
+// The lane kernel (rs_lane.hip) stages the 8-word basis images of its tables
+// when 1 (the host, rs_codec.cpp try_lane, hands it the matching images), the
+// 16-word images when 0.
+#ifndef RS_LANE_BASIS
+#define RS_LANE_BASIS 1
+#endif
 enum MonoMode {
     kMonoEncodeHigh = 0,
     kMonoEncodeLow = 1,

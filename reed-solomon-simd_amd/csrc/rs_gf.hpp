@@ -82,6 +82,20 @@ __device__ __forceinline__ void gf_muladd4(uint32_t &acc_l, uint32_t &acc_h, uin
     acc_h = xor3(acc_h, ha, hb);
 }
 
+// Two pieces (fields f, f + 1) of a 16-word 2-element table from one 16-byte piece
+// (A_f, C_f, A_f+1, C_f+1) of its 8-word basis (rs_codec.cpp basis_images): field
+// f's four lookups are {0, a, b, a ^ b}, so A = a | b << 16 gives the table words
+// [0, a_lo, b_lo, (a^b)_lo] and [0, a_hi, b_hi, (a^b)_hi] (gf_tables.cpp fill_perm2).
+__device__ __forceinline__ void basis2_expand(const uint4 &v, uint4 &a, uint4 &b) {
+    auto field = [](uint32_t A, uint32_t C) {
+        const uint32_t tA = A ^ __builtin_amdgcn_alignbit(A, A, 16), tC = C ^ __builtin_amdgcn_alignbit(C, C, 16);
+        return uint4{__builtin_amdgcn_perm(tA, A, 0x0402000Cu), __builtin_amdgcn_perm(tC, C, 0x0503010Cu),
+                     __builtin_amdgcn_perm(tC, C, 0x0402000Cu), __builtin_amdgcn_perm(tA, A, 0x0503010Cu)};
+    };
+    a = field(v.x, v.y);
+    b = field(v.z, v.w);
+}
+
 // The 20-word table of a multiplier from its 8-word basis (rs_codec.cpp
 // basis_images / basis tables): multiplication by a constant is GF(2)-linear, so
 // a 3-bit field's 8 lookups are [0, p0, p1, p0^p1] and that word XOR p2

@@ -21,7 +21,8 @@
 //   IFFT layers 0..5 in A (wave-private tables), one LDS remap,
 //   IFFT layers 6..L-1 and FFT layers L-1..L-6 in B (tables shared by the waves),
 //   one LDS remap, FFT layers L-7..0 in A (wave-private tables).
-// Every table of the launch is staged in LDS at the start: 16-byte pieces,
+// Every table of the launch is staged in LDS at the start, built from its 8-word
+// basis (rs_codec.cpp basis_images, rs_gf.hpp basis2_expand): 16-byte pieces,
 // piece-major per region (position piece * 68 + slot: the two lanes of a
 // butterfly read pieces {0, 1} and {2, 3} of one table, 68 = 4 mod 16 spreads
 // them over the banks).
@@ -197,12 +198,28 @@ __global__ void __launch_bounds__(1 << L) k_lane(const MonoCore A) {
                         : *reinterpret_cast<const uint32_t *>(a - (reinterpret_cast<uintptr_t>(a) & 3u));
     }
 
-    // ---- table staging loads: 16-byte pieces of the images (slot-major there)
+    // ---- table staging loads: 16-byte pieces of the basis images (rs_codec.cpp
+    // basis_images: 2 per table, slot-major), built into the table's 4 pieces while
+    // written (basis2_expand; half the staging's L2 requests)
+    // (RS_LANE_BASIS=0: the 16-word images, 4 pieces per table, copied as they are)
+    constexpr uint32_t P = RS_LANE_BASIS ? 2 : 4;  // image pieces per table
     auto img_piece = [](const uint32_t *img, uint32_t slot, uint32_t piece) {
-        return reinterpret_cast<const uint4 *>(img)[slot * 4u + piece];
+        return reinterpret_cast<const uint4 *>(img)[slot * P + piece];
     };
-    constexpr int K1 = (4 * G::kA1 + 63) / 64, K3 = (4 * G::kA3 + 63) / 64;
-    constexpr uint32_t kShP = 4 * (G::kShI + G::kShF);
+    // write image piece h of table slot s into the planes at `base` (basis piece h:
+    // table pieces 2h, 2h + 1)
+    auto put = [&](uint32_t base, uint32_t s, uint32_t h, const uint4 &v) {
+        if constexpr (P == 2) {
+            uint4 a, b;
+            basis2_expand(v, a, b);
+            *reinterpret_cast<uint4 *>(lds8 + base + ((2u * h) * G::NT + s) * 16u) = a;
+            *reinterpret_cast<uint4 *>(lds8 + base + ((2u * h + 1u) * G::NT + s) * 16u) = b;
+        } else {
+            *reinterpret_cast<uint4 *>(lds8 + base + (h * G::NT + s) * 16u) = v;
+        }
+    };
+    constexpr int K1 = (P * G::kA1 + 63) / 64, K3 = (P * G::kA3 + 63) / 64;
+    constexpr uint32_t kShP = P * (G::kShI + G::kShF);
     constexpr int KS = (kShP + n - 1) / n;
     uint4 v1[K1], v3[K3], vs[KS];
     // phase-A regions: region slot t = layer x's first slot + g (g < 32 >> x) holds the
@@ -210,9 +227,9 @@ __global__ void __launch_bounds__(1 << L) k_lane(const MonoCore A) {
 #pragma unroll
     for (int k = 0; k < K1; ++k) {
         uint32_t q = lane + 64u * k;
-        q = q < 4 * G::kA1 ? q : 4 * G::kA1 - 1;
-        const uint32_t t = q >> 2, x = a_layer(t);
-        v1[k] = img_piece(img_i, n - (n >> x) + wave * (32u >> x) + t - (64u - (64u >> x)), q & 3u);
+        q = q < P * G::kA1 ? q : P * G::kA1 - 1;
+        const uint32_t t = q / P, x = a_layer(t);
+        v1[k] = img_piece(img_i, n - (n >> x) + wave * (32u >> x) + t - (64u - (64u >> x)), q % P);
     }
     // the shared and the phase-A FFT tables, also up front (requested during the
     // phase-A IFFT instead: 2^8 rows 4.35 -> 4.70 us, 2^9 5.50 -> 5.77 us, 2^10
@@ -222,17 +239,17 @@ __global__ void __launch_bounds__(1 << L) k_lane(const MonoCore A) {
         for (int k = 0; k < KS; ++k) {
             uint32_t q = tid + n * k;
             q = q < kShP ? q : kShP - 1;
-            const uint32_t t = q >> 2;
+            const uint32_t t = q / P;
             // shared IFFT: image slots n - n/64 .. (layers 6..L-1); shared FFT: n - n/2^WB ..
-            vs[k] = t < G::kShI ? img_piece(img_i, n - (n >> 6) + t, q & 3u)
-                                : img_piece(img_f, n - (n >> G::WB) + (t - G::kShI), q & 3u);
+            vs[k] = t < G::kShI ? img_piece(img_i, n - (n >> 6) + t, q % P)
+                                : img_piece(img_f, n - (n >> G::WB) + (t - G::kShI), q % P);
         }
 #pragma unroll
         for (int k = 0; k < K3; ++k) {
             uint32_t q = lane + 64u * k;
-            q = q < 4 * G::kA3 ? q : 4 * G::kA3 - 1;
-            const uint32_t t = q >> 2, x = a_layer(t);
-            v3[k] = img_piece(img_f, n - (n >> x) + wave * (32u >> x) + t - (64u - (64u >> x)), q & 3u);
+            q = q < P * G::kA3 ? q : P * G::kA3 - 1;
+            const uint32_t t = q / P, x = a_layer(t);
+            v3[k] = img_piece(img_f, n - (n >> x) + wave * (32u >> x) + t - (64u - (64u >> x)), q % P);
         }
     }
     RS_LSTAMP(1);
@@ -251,8 +268,7 @@ __global__ void __launch_bounds__(1 << L) k_lane(const MonoCore A) {
 #pragma unroll
     for (int k = 0; k < K1; ++k) {
         const uint32_t q = lane + 64u * k;
-        if (q < 4 * G::kA1)
-            *reinterpret_cast<uint4 *>(lds8 + a1 + ((q & 3u) * G::NT + (q >> 2)) * 16u) = v1[k];
+        if (q < P * G::kA1) put(a1, q / P, q % P, v1[k]);
     }
     RS_LSTAMP(2);
     // the column: rows outside the caller's matrices are zero
@@ -297,17 +313,15 @@ __global__ void __launch_bounds__(1 << L) k_lane(const MonoCore A) {
             for (int i = 0; i < KS; ++i) {
                 const uint32_t q = tid + n * i;
                 if (q < kShP) {
-                    const uint32_t t = q >> 2;
+                    const uint32_t t = q / P;
                     const uint32_t base = t < G::kShI ? G::kShIBase : G::kShFBase;
-                    const uint32_t s = t < G::kShI ? t : t - G::kShI;
-                    *reinterpret_cast<uint4 *>(lds8 + base + ((q & 3u) * G::NT + s) * 16u) = vs[i];
+                    put(base, t < G::kShI ? t : t - G::kShI, q % P, vs[i]);
                 }
             }
 #pragma unroll
             for (int i = 0; i < K3; ++i) {
                 const uint32_t q = lane + 64u * i;
-                if (q < 4 * G::kA3)
-                    *reinterpret_cast<uint4 *>(lds8 + a3 + ((q & 3u) * G::NT + (q >> 2)) * 16u) = v3[i];
+                if (q < P * G::kA3) put(a3, q / P, q % P, v3[i]);
             }
             RS_LSTAMP(4);
             remap(row_a, row_b);  // (its barriers also publish the shared tables)

@@ -334,15 +334,6 @@ struct GlobalTabs {
 // 2^11 rows 1 % 13.47 / 13.42 -> 13.63 / 13.62 us (profiles/r05h/basis_ab.txt), so
 // RS_MONO_BASIS (rs_device.hpp) is off: 1 builds k_mono with it (the host then
 // hands it basis images, rs_codec.cpp mono_args).
-__device__ __forceinline__ void basis_expand(const uint4 &v, uint4 &a, uint4 &b) {
-    auto field = [](uint32_t A, uint32_t C) {
-        const uint32_t tA = A ^ __builtin_amdgcn_alignbit(A, A, 16), tC = C ^ __builtin_amdgcn_alignbit(C, C, 16);
-        return uint4{__builtin_amdgcn_perm(tA, A, 0x0402000Cu), __builtin_amdgcn_perm(tC, C, 0x0503010Cu),
-                     __builtin_amdgcn_perm(tC, C, 0x0402000Cu), __builtin_amdgcn_perm(tA, A, 0x0503010Cu)};
-    };
-    a = field(v.x, v.y);
-    b = field(v.z, v.w);
-}
 
 template <int L, int LR, int SP = 0, int E = 4>
 struct Stage {
@@ -358,7 +349,7 @@ struct Stage {
         if constexpr (kBasis) {
             const uint32_t p0 = (q >> 1) * PC + (q & 1u) * 2u;  // table piece of field 2 (q & 1)
             uint4 a, b;
-            basis_expand(v, a, b);
+            basis2_expand(v, a, b);
             reinterpret_cast<uint4 *>(region)[at(p0)] = a;
             reinterpret_cast<uint4 *>(region)[at(p0 + 1)] = b;
         } else {

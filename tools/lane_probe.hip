@@ -28,7 +28,8 @@ int main(int argc, char **argv) {
     uint32_t L = 0;
     while ((1u << L) < n) ++L;
     const auto &T = rs::tables();
-    const int tw = rs::kPerm2Words;
+    // RS_LANE_BASIS: 8-word basis images (rs_codec.cpp basis_images), else the 16-word tables
+    const int tw = RS_LANE_BASIS ? 8 : rs::kPerm2Words;
     const uint32_t nimg = 65536u / n;
     const size_t words = size_t(n - 1) * tw;
     std::vector<uint32_t> h(words * nimg);
@@ -36,7 +37,17 @@ int main(int argc, char **argv) {
         for (uint32_t b = 0; b < L; ++b)
             for (uint32_t g = 0; g < (n >> (b + 1)); ++g) {
                 const uint32_t slot = n - (n >> b) + g, idx = (g << (b + 1)) + (1u << b) + t * n - 1;
-                std::copy_n(&T.perm2_by_skew[size_t(idx) * tw], tw, &h[t * words + size_t(slot) * tw]);
+                uint32_t *dst = &h[t * words + size_t(slot) * tw];
+                if (RS_LANE_BASIS) {
+                    const uint16_t lm = T.skew[idx];
+                    auto P = [&](int i) -> uint32_t { return lm == 65535 ? 0u : T.mul(uint16_t(1u << i), lm); };
+                    for (int f = 0; f < 4; ++f) {
+                        dst[2 * f] = P(2 * f) | (P(2 * f + 1) << 16);
+                        dst[2 * f + 1] = P(8 + 2 * f) | (P(9 + 2 * f) << 16);
+                    }
+                } else {
+                    std::copy_n(&T.perm2_by_skew[size_t(idx) * tw], tw, dst);
+                }
             }
     uint32_t *d_img;
     CK(hipMalloc(&d_img, h.size() * 4));
@@ -44,7 +55,12 @@ int main(int argc, char **argv) {
     uint8_t *orig, *rec;
     CK(hipMalloc(&orig, size_t(n) * S));
     CK(hipMalloc(&rec, size_t(n) * S));
-    CK(hipMemset(orig, 0x37, size_t(n) * S));
+    {
+        std::vector<uint8_t> hin(size_t(n) * S);
+        uint32_t x = 12345;
+        for (auto &c : hin) c = uint8_t((x = x * 1103515245u + 12345u) >> 16);
+        CK(hipMemcpy(orig, hin.data(), hin.size(), hipMemcpyHostToDevice));
+    }
     rs::MonoArgs A;
     A.elems = 2;
     A.packs = S / 4;
@@ -71,7 +87,12 @@ int main(int argc, char **argv) {
     CK(hipEventSynchronize(e1));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
-    printf("k_lane<%u> %u:%u x %u: %.3f us per launch back to back\n", L, n, n, S, ms * 1e3f / reps);
+    std::vector<uint32_t> out(size_t(n) * S / 4);
+    CK(hipMemcpy(out.data(), rec, out.size() * 4, hipMemcpyDeviceToHost));
+    uint64_t hsh = 1469598103934665603ull;
+    for (uint32_t w : out) hsh = (hsh ^ w) * 1099511628211ull;
+    printf("k_lane<%u> (basis %d) %u:%u x %u: %.3f us per launch back to back, output hash %016llx\n", L, RS_LANE_BASIS, n, n,
+           S, ms * 1e3f / reps, (unsigned long long)hsh);
 #ifdef RS_LANE_STAMPS
     CK(rs::launch_lane(int(L), A, s));
     CK(hipStreamSynchronize(s));
