@@ -201,12 +201,29 @@ __device__ __forceinline__ void c_xpose(CRows<PW> &r, uint32_t lane) {
     });
 }
 
-// IFFT layers 0..L-1 (engine_naive.rs:75-105), placement as in the header
+// Top layer of a transform with skew offset 0 (zero twiddle, rs_mono.hip
+// run_seq zero_top): both butterflies reduce to b ^= a.
+template <int E, int PW>
+__device__ __forceinline__ void c_xor_layer(CRows<PW> &r) {
+    static_for<0, PW>([&](auto pc) {
+        r.lo[pc][1] ^= r.lo[pc][0];
+        if constexpr (E == 4) r.hi[pc][1] ^= r.hi[pc][0];
+    });
+}
+
+// IFFT layers 0..L-1 (engine_naive.rs:75-105), placement as in the header;
+// zero_top: skew offset 0
 template <int L, int E, int PW>
-__device__ __forceinline__ void c_ifft(CRows<PW> &r, const uint32_t *region, uint32_t lane) {
+__device__ __forceinline__ void c_ifft(CRows<PW> &r, const uint32_t *region, uint32_t lane, bool zero_top = false) {
     static_for<0, L>([&](auto bc) {
         constexpr int B = decltype(bc)::value;
         if constexpr (B > 0) c_xpose<B - 1, E>(r, lane);
+        if constexpr (B == L - 1 && RS_MONO_ZERO_TOP) {
+            if (zero_top) {
+                c_xor_layer<E>(r);
+                return;
+            }
+        }
         uint32_t t[ChunkGeo<L, E>::TW];
         c_table<L, E, B>(region, lane, t);
         static_for<0, PW>([&](auto pc) {
@@ -218,10 +235,16 @@ __device__ __forceinline__ void c_ifft(CRows<PW> &r, const uint32_t *region, uin
 
 // FFT layers L-1..0 (engine_naive.rs:43-73)
 template <int L, int E, int PW>
-__device__ __forceinline__ void c_fft(CRows<PW> &r, const uint32_t *region, uint32_t lane) {
+__device__ __forceinline__ void c_fft(CRows<PW> &r, const uint32_t *region, uint32_t lane, bool zero_top = false) {
     static_for<0, L>([&](auto ic) {
         constexpr int B = L - 1 - decltype(ic)::value;
         if constexpr (B < L - 1) c_xpose<B, E>(r, lane);
+        if constexpr (B == L - 1 && RS_MONO_ZERO_TOP) {
+            if (zero_top) {
+                c_xor_layer<E>(r);
+                return;
+            }
+        }
         uint32_t t[ChunkGeo<L, E>::TW];
         c_table<L, E, B>(region, lane, t);
         static_for<0, PW>([&](auto pc) {
@@ -392,7 +415,7 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_chunks(const MonoCore A) {
                 });
             });
         tabs.write(region, lane);
-        c_fft<L, E>(acc, region, lane);
+        c_fft<L, E>(acc, region, lane, A.fft_img == 0);
         RS_CSTAMP(5);
         c_store_chunk<L, E>(A.dst, 0, io, ok, lane, acc);
         RS_CSTAMP(6);
@@ -406,7 +429,7 @@ __global__ void __launch_bounds__(64 * kMaxWaves) k_chunks(const MonoCore A) {
         uint32_t c = wave;
         tabs.issue(img_base + uint64_t(A.fft_img + c * A.fft_img_step) * A.img_words, lane);  // in flight during the IFFT
         RS_CSTAMP(1);
-        c_ifft<L, E>(x, region, lane);
+        c_ifft<L, E>(x, region, lane, A.ifft_img == 0);
         RS_CSTAMP(2);
         while (c < A.chunks) {
             tabs.write(region, lane);

@@ -200,6 +200,11 @@ char *launch_name_buf();
 // The lane kernel (rs_lane.hip) stages the 8-word basis images of its tables
 // when 1 (the host, rs_codec.cpp try_lane, hands it the matching images), the
 // 16-word images when 0.
+// Column kernels skip the multiply of a top layer whose twiddle is zero (skew
+// offset 0: rs_mono.hip run_seq zero_top) when 1.
+#ifndef RS_MONO_ZERO_TOP
+#define RS_MONO_ZERO_TOP 1
+#endif
 #ifndef RS_LANE_BASIS
 #define RS_LANE_BASIS 1
 #endif

@@ -336,7 +336,14 @@ __global__ void __launch_bounds__(1 << L) k_lane(const MonoCore A) {
             if constexpr (k + 1 < 2 * L) request(std::integral_constant<int, k + 1>{});
         }
 #ifndef RS_LANE_SKIP_LAYERS  // tools/lane_probe.hip ablation
-        lane_layer<J, Q::ifft(k)>(v, tb[k & 1], rm[J], sh[J]);
+        if constexpr (Q::bit(k) == L - 1 && RS_MONO_ZERO_TOP) {
+            // skew offset 0 (image 0): the top layer's twiddle is zero (rs_mono.hip
+            // run_seq zero_top), both butterflies reduce to b ^= a
+            if ((Q::ifft(k) ? A.ifft_img : A.fft_img) == 0) v ^= partner<J>(v, rm[J]) & rm[J];
+            else lane_layer<J, Q::ifft(k)>(v, tb[k & 1], rm[J], sh[J]);
+        } else {
+            lane_layer<J, Q::ifft(k)>(v, tb[k & 1], rm[J], sh[J]);
+        }
 #else
         v ^= tb[k & 1][0] ^ tb[k & 1][7];
 #endif

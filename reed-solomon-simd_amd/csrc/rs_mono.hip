@@ -558,6 +558,21 @@ __device__ __forceinline__ void apply_remap(Col<L, LR, E> &c, uint32_t *plane, u
     });
 }
 
+// Layer with a zero twiddle (m = 0: engine_naive.rs:64-68 / 96-100 skip the
+// multiply, log_m == GF_MODULUS): both butterflies reduce to b ^= a.
+template <int L, int LR, typename S, int I, int E>
+__device__ __forceinline__ void apply_xor_layer(Col<L, LR, E> &c) {
+    constexpr Op op = S::v.ops[I];
+    static_for<0, (1 << LR)>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int i2 = i | (1 << op.rs);
+        if constexpr (!((i >> op.rs) & 1)) {
+            c.lo[i2] ^= c.lo[i];
+            if constexpr (Fmt<E>::kHi) c.hi[i2] ^= c.hi[i];
+        }
+    });
+}
+
 constexpr int layer_at(const Seq &s, int k) {
     for (int i = 0; i < s.count; ++i)
         if (s.ops[i].kind == kOpLayer && k-- == 0) return i;
@@ -583,12 +598,14 @@ struct NoHook {
 // tables of layer ordinal KHOOK are requested (the staged kernel writes a
 // wave-private table region there that the layers before it have read).  A
 // wave with `pre` false skips the ops before the remap, with `alive` false
-// the ops after it.
+// the ops after it.  zero_top: the transform's skew offset is 0 (image 0), so
+// the single twiddle of its top layer L-1 is skew[2^(L-1) - 1] = GF_MODULUS
+// (tables.rs:285-324: the 16 such entries are skew[2^b - 1]), a multiply-free layer.
 template <int L, int LR, bool FFT, int B0, int KHOOK = -1, int SPLIT = 0, typename TS, typename PreRemap,
           int E, typename Hook = NoHook>
 __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR, E> &c, uint32_t *plane, uint32_t lane, uint32_t wave,
                                         const PreRemap &pre_remap, bool alive = true, bool pre = true,
-                                        const Hook &hook = Hook{}) {
+                                        const Hook &hook = Hook{}, bool zero_top = false) {
     using S = SeqOf<L, LR, FFT, SPLIT>;
     constexpr int NT = (1 << LR) / 2;
     constexpr int NL = num_layers(S::v);
@@ -625,7 +642,12 @@ __device__ __forceinline__ void run_seq(const TS &ts, Col<L, LR, E> &c, uint32_t
         } else {
             constexpr int k = layer_ordinal(S::v, I);
 #ifndef RS_MONO_SKIP_LAYERS
-            apply_layer<L, LR, S, I, !FFT, E>(tb[k % B], c);
+            if constexpr (op.bit == L - 1 && RS_MONO_ZERO_TOP) {
+                if (zero_top) apply_xor_layer<L, LR, S, I, E>(c);
+                else apply_layer<L, LR, S, I, !FFT, E>(tb[k % B], c);
+            } else {
+                apply_layer<L, LR, S, I, !FFT, E>(tb[k % B], c);
+            }
 #endif
             constexpr int end = k < NL1 ? NL1 : NL;
             if constexpr (k + B < end) {
@@ -1102,10 +1124,14 @@ __device__ __forceinline__ void fd_in_wave(const uint32_t (&vl)[1 << LR], const 
 // Only the waves of the half `out_half` (the one holding restored rows) go on
 // with the FFT; they compute both halves' values of their row positions, so
 // the other half's waves only hand over their rows.  Three barriers; every
-// wave reaches them.
+// wave reaches them.  zi / zf: the IFFT's / FFT's skew offset is 0, so mI / mF
+// is zero (run_seq zero_top) and its layer needs no multiply.
 template <int L, int LR, int E>
 __device__ __forceinline__ void split_top(Col<L, LR, E> &c, uint32_t *plane, uint32_t *plane2, const uint32_t *tab_i,
-                                          const uint32_t *tab_f, uint32_t lane, uint32_t wave, uint32_t out_half) {
+                                          const uint32_t *tab_f, uint32_t lane, uint32_t wave, uint32_t out_half,
+                                          bool zi = false, bool zf = false) {
+    zi = zi && RS_MONO_ZERO_TOP;
+    zf = zf && RS_MONO_ZERO_TOP;
     using S = SeqOf<L, LR, true, true>;
     constexpr bool HI = Fmt<E>::kHi;
     constexpr int TW = Fmt<E>::kTW;
@@ -1146,6 +1172,11 @@ __device__ __forceinline__ void split_top(Col<L, LR, E> &c, uint32_t *plane, uin
                 const uint32_t ph = plane[n + x];
                 lh[i] = out_half ? ph : c.hi[i];
                 uh[i] = out_half ? c.hi[i] : ph;
+            }
+            if (zi) {
+                ul[i] ^= ll[i];
+                if constexpr (HI) uh[i] ^= lh[i];
+            } else if constexpr (HI) {
                 ifft_bfly(ll[i], lh[i], ul[i], uh[i], ti);
             } else {
                 ifft_bfly2(ll[i], ul[i], ti);
@@ -1185,13 +1216,16 @@ __device__ __forceinline__ void split_top(Col<L, LR, E> &c, uint32_t *plane, uin
         static_for<0, R>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             fl[i] ^= ul[i];  // bit L-1 term: lower rows take their upper partner (pre-derivative)
-            if constexpr (HI) {
-                fh[i] ^= uh[i];
+            if constexpr (HI) fh[i] ^= uh[i];
+            if (zf) {
+                gl[i] ^= fl[i];
+                if constexpr (HI) gh[i] ^= fh[i];
+            } else if constexpr (HI) {
                 fft_bfly(fl[i], fh[i], gl[i], gh[i], tf);
-                c.hi[i] = out_half ? gh[i] : fh[i];
             } else {
                 fft_bfly2(fl[i], gl[i], tf);
             }
+            if constexpr (HI) c.hi[i] = out_half ? gh[i] : fh[i];
             c.lo[i] = out_half ? gl[i] : fl[i];
         });
     }
@@ -1835,7 +1869,7 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 const bool alive = out && wave_stores<L, LR, PK>(A, wave);
                 constexpr uint32_t kTopI = (G::n >> G::IW) - 2, kTopF = G::kShI + (G::n >> G::FLO) - 2;
                 split_top<L, LR>(c, plane, lds + G::words_dec, shared + kTopI * G::SW, shared + kTopF * G::SW, lane, wave,
-                                 A.out_half);
+                                 A.out_half, ii == 0, fi == 0);
                 RS_MSTAMP(6);
                 issue4(alive);
                 // FFT below the top layer: only the half that holds restored rows
@@ -1884,11 +1918,11 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 const bool alive = !HFD || wave_stores<L, LR, PK>(A, wave, hh << L);
                 issue4(alive);
                 run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, PK>(ts, c, plane, lane, wave, pre3(alive),
-                                                                                alive, true, write4);
+                                                                                alive, true, write4, fi == 0);
                 if (!alive) return;
             } else if constexpr (G::WB > 0) {
                 run_seq<L, LR, false, RS_MONO_LDS_PF, G::B0 ? 1 : -1, PK>(ts, c, plane, lane, wave, issue3, true, live,
-                                                                       write1);
+                                                                       write1, ii == 0);
                 if constexpr (HALF_I) {  // the half's IFFT rows to the work rows; no FFT here
                     store_col<L, LR, false, PK, E, true>(A, ri, hh, io_w, sb, c, lane, wave);
                     RS_MSTAMP(11);
@@ -1901,15 +1935,17 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 issue4(alive);  // (waves that stop early all read one table: no branch around the loads)
                 if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
                 run_seq<L, LR, true, RS_MONO_LDS_PF, G::B0 ? NLF - 1 : -1, PK>(ts, c, plane, lane, wave, pre3(alive), alive,
-                                                                            true, write4);
+                                                                            true, write4, fi == 0);
                 if (!alive) return;
             } else {
                 static_assert(!G::B0, "one-segment plans keep every table in the region");
-                run_seq<L, LR, false, RS_MONO_LDS_PF, -1, PK>(ts, c, plane, lane, wave, NoHook{});
+                run_seq<L, LR, false, RS_MONO_LDS_PF, -1, PK>(ts, c, plane, lane, wave, NoHook{}, true, true, NoHook{},
+                                                              ii == 0);
                 issue3();
                 if constexpr (DEC) formal_derivative<L, LR>(c, plane, lane, wave);
                 write3();
-                run_seq<L, LR, true, RS_MONO_LDS_PF, -1, PK>(ts, c, plane, lane, wave, NoHook{});
+                run_seq<L, LR, true, RS_MONO_LDS_PF, -1, PK>(ts, c, plane, lane, wave, NoHook{}, true, true, NoHook{},
+                                                             fi == 0);
             }
             RS_MSTAMP(10);
             store_col<L, LR, DEC || HFD, PK>(A, ri, HALF_F ? hh : 0u, io, sb, c, lane, wave,

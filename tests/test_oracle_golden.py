@@ -70,6 +70,22 @@ def test_tables_invariants():
     assert exp[65535] == exp[0] == 1
 
 
+def test_zero_twiddles_are_the_skew_offset_0_top_layers():
+    """The premise of the kernels' multiply-free top layers (RS_MONO_ZERO_TOP,
+    rs_mono.hip run_seq zero_top): the skew table (tables.rs:285-324) holds
+    GF_MODULUS (a zero twiddle) exactly at skew[2^b - 1], the single twiddle of
+    layer b of a transform at skew offset 0; so an image-0 transform of 2^L rows
+    has a zero-twiddle top layer and every offset n*t > 0 none."""
+    skew = O.table("skew", 65535)
+    zeros = np.flatnonzero(skew == 65535)
+    assert zeros.tolist() == [(1 << b) - 1 for b in range(16)]
+    for L in range(1, 16):
+        n = 1 << L
+        top = [(n >> 1) - 1 + t * n for t in range(65536 // n)]
+        assert skew[top[0]] == 65535
+        assert all(skew[i] != 65535 for i in top[1:])
+
+
 def test_formal_derivative_closed_form():
     """utils.rs:99-104 equals out[q] = in[q] ^ XOR_{b: q_b=0, 2^b<n} in[q|2^b]."""
     rng = np.random.default_rng(1)

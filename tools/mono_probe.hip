@@ -70,7 +70,13 @@ int main(int argc, char **argv) {
     uint8_t *orig, *rec;
     CK(hipMalloc(&orig, size_t(n) * S));
     CK(hipMalloc(&rec, size_t(n) * S));
-    CK(hipMemset(orig, 0x37, size_t(n) * S));
+    {
+        std::vector<uint8_t> hin(size_t(n) * S);
+        uint32_t x = 12345;
+        for (auto &c : hin) c = uint8_t((x = x * 1103515245u + 12345u) >> 16);
+        CK(hipMemcpy(orig, hin.data(), hin.size(), hipMemcpyHostToDevice));
+    }
+    CK(hipMemset(rec, 0, size_t(n) * S));
     rs::MonoArgs A;
     A.elems = e2 ? 2 : 4;
     A.packs = e2 ? S / 4 : S / 8;
@@ -162,8 +168,14 @@ int main(int argc, char **argv) {
     CK(hipEventSynchronize(b));
     float ms;
     CK(hipEventElapsedTime(&ms, a, b));
-    printf("mono %s%s%s n=%u S=%u: %.2f us/launch (back-to-back)\n", dec ? "decode" : "encode", A.split ? " split" : "", e2 ? " e2" : "", n,
-           S, ms * 1000 / iters);
+    uint64_t hsh = 1469598103934665603ull;
+    {  // output hash (A/B builds must agree)
+        std::vector<uint32_t> out(size_t(n) * S / 4);
+        CK(hipMemcpy(out.data(), rec, out.size() * 4, hipMemcpyDeviceToHost));
+        for (uint32_t w : out) hsh = (hsh ^ w) * 1099511628211ull;
+    }
+    printf("mono %s%s%s n=%u S=%u: %.2f us/launch (back-to-back), output hash %016llx\n", dec ? "decode" : "encode",
+           A.split ? " split" : "", e2 ? " e2" : "", n, S, ms * 1000 / iters, (unsigned long long)hsh);
     {  // floor: an empty kernel with the same grid, block and LDS
         const size_t lds = size_t(rs::Stage<10, 1>::words_dec) * 4;
         CK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_empty_lds), hipFuncAttributeMaxDynamicSharedMemorySize,
