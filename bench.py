@@ -50,6 +50,10 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 METRIC = "GiB/s (original+recovery) encode & decode, device-resident, 1024:1024×1024B"
 HBM_PEAK_GBS = 8000.0
 SIMDS, CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 2  # MI355X: 256 CUs x 4 SIMDs; a wave64 VALU op issues over 2 cycles
+# measured issue cost of the GF multiply mixes (gf_muladd2 / gf_muladd4: all VOP3 but a few
+# ANDs) at 4 waves per SIMD, in 2.4 GHz clocks per wave64 instruction per SIMD
+# (tools/valu_rate.hip, profiles/r05j/valu_rate.txt: VOP3 4.3, VOP2 2.6, the mixes 4.0)
+VALU_MIX_CYCLES = 4.0
 
 CONFIGS = {
     # name: (original_count, recovery_count, shard_bytes)
@@ -288,8 +292,11 @@ def roofline_of(rs, ctx, fn, profile_steps, alg_step_bytes, config, launch_scope
     if "valu" in pmc:
         insts = pmc["valu"][0]
         valu = {"valu_insts_per_launch": insts, "frac": round(insts * VALU_CYCLES / (dom_avg_s * CLOCK_HZ * SIMDS), 4),
+                "issue_frac": round(insts * VALU_MIX_CYCLES / (dom_avg_s * CLOCK_HZ * SIMDS), 4),
                 "source": pmc["valu"][1],
-                "note": "SQ_INSTS_VALU x 2 cycles per wave-instruction / (launch duration x 1024 SIMDs x 2.4 GHz)"}
+                "note": "frac: SQ_INSTS_VALU x 2 cycles per wave-instruction / (launch duration x 1024 SIMDs x "
+                        "2.4 GHz); issue_frac: x the measured 4.0 cycles of the GF multiply mix instead "
+                        "(tools/valu_rate.hip)"}
     return {"bound": "hbm", "kernel": dom, "scope": scope, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": pmc["traffic"][0] if "traffic" in pmc else None,

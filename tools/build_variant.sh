@@ -9,7 +9,7 @@ PKG=reed-solomon-simd_amd
 B=$PKG/build/variant_$NAME
 mkdir -p "$B" $PKG/lib/variants
 objs=()
-for src in rs_kernels.hip rs_mono.hip rs_eval.hip rs_codec.cpp gf_tables.cpp; do
+for src in rs_kernels.hip rs_mono.hip rs_lane.hip rs_chunks.hip rs_eval.hip rs_codec.cpp gf_tables.cpp; do
   if [[ " $SRCS " == *" $src "* ]]; then
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c $PKG/csrc/$src -o $B/$src.o
     objs+=($B/$src.o)
