@@ -172,7 +172,12 @@ enum PassFlags {
     kFd = 32,
     kXorIn = 64,
     kReveal = 128,
-    kEval = 256  // fused eval_poly (PassArgs::fused_eval)
+    kEval = 256,  // fused eval_poly (PassArgs::fused_eval)
+    // the IFFT's / FFT's local layer K-1 has a zero twiddle: the pass holds the
+    // transform's top bit and its skew offset is 0 for every chunk of the launch
+    // (rs_kernels.hip launch_k; the variants that have them)
+    kZeroI = 512,
+    kZeroF = 1024
 };
 
 // Launch one pass on `stream`.  K = log2(rows per set).

@@ -533,6 +533,21 @@ __device__ __forceinline__ void layer(const Ctx &c, const uint32_t *tab, uint32_
     });
 }
 
+// A layer whose twiddle is zero (the top layer of a transform at skew offset 0,
+// kZeroI / kZeroF; rs_mono.hip run_seq zero_top): both butterflies reduce to b ^= a.
+template <int K, int LR, int SPL, int PH, int B>
+__device__ __forceinline__ void xor_layer(uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
+    using P = Pass<K, LR, SPL>;
+    constexpr int RB = B - P::start(PH);
+    static_for<0, P::R>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (!((i >> RB) & 1)) {
+            lo[i | (1 << RB)] ^= lo[i];
+            hi[i | (1 << RB)] ^= hi[i];
+        }
+    });
+}
+
 // 2x2 transpose between lane rows 16 (LANE_BIT 4) or 32 (LANE_BIT 5) apart:
 // the lane with lane bit clear keeps a and takes its partner's a as b, the
 // partner keeps b and takes the a-lane's b as a (v_permlane{16,32}_swap).
@@ -679,7 +694,8 @@ __device__ __forceinline__ void apply_layer(const LayerTabs<LR> &T, uint32_t (&l
 // Narrow shapes (<= 4 rows per lane) read layer n+1's tables into registers
 // while layer n runs, so the LDS latency hides behind the butterflies and
 // the phase exchanges; wide shapes read one table at a time (registers).
-template <int K, int LR, int SPL, bool IFFT>
+// ZT: layer K-1 has a zero twiddle (kZeroI / kZeroF): no table, no multiply.
+template <int K, int LR, int SPL, bool IFFT, bool ZT = false>
 __device__ __forceinline__ void transform(const Ctx &c, uint32_t *plane, const uint32_t *tab,
                                           uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
     using P = Pass<K, LR, SPL>;
@@ -694,23 +710,25 @@ __device__ __forceinline__ void transform(const Ctx &c, uint32_t *plane, const u
             constexpr int ph = P::phase_of(b);
             if constexpr (n > 0 && P::phase_of(prev) != ph)
                 exchange<K, LR, SPL, P::phase_of(prev), ph>(c, plane, lo, hi);
-            layer<K, LR, SPL, ph, b, IFFT>(c, tab, lo, hi);
+            if constexpr (ZT && b == K - 1) xor_layer<K, LR, SPL, ph, b>(lo, hi);
+            else layer<K, LR, SPL, ph, b, IFFT>(c, tab, lo, hi);
         });
     } else {
         LayerTabs<LR> T[2];
         constexpr int b0 = IFFT ? 0 : K - 1;
-        read_tables<K, LR, SPL, P::phase_of(b0), b0>(c, tab, T[0]);
+        if constexpr (!(ZT && b0 == K - 1)) read_tables<K, LR, SPL, P::phase_of(b0), b0>(c, tab, T[0]);
         static_for<0, K>([&](auto bc) {
             constexpr int n = decltype(bc)::value;
             constexpr int b = IFFT ? n : K - 1 - n;
             constexpr int prev = IFFT ? b - 1 : b + 1;
             constexpr int next = IFFT ? b + 1 : b - 1;
             constexpr int ph = P::phase_of(b);
-            if constexpr (n + 1 < K)
+            if constexpr (n + 1 < K && !(ZT && next == K - 1))
                 read_tables<K, LR, SPL, P::phase_of(next), next>(c, tab, T[(n + 1) & 1]);
             if constexpr (n > 0 && P::phase_of(prev) != ph)
                 exchange<K, LR, SPL, P::phase_of(prev), ph>(c, plane, lo, hi);
-            apply_layer<K, LR, SPL, ph, b, IFFT>(T[n & 1], lo, hi);
+            if constexpr (ZT && b == K - 1) xor_layer<K, LR, SPL, ph, b>(lo, hi);
+            else apply_layer<K, LR, SPL, ph, b, IFFT>(T[n & 1], lo, hi);
         });
     }
 }
@@ -796,7 +814,9 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
     constexpr bool XOR_IN = FLAGS & kXorIn;        // decode: x ^= rows of A.xor_in
     constexpr bool REVEAL = FLAGS & kReveal;       // decode: store erased originals, unscaled
     constexpr bool EVAL = FLAGS & kEval;           // decode: eval_poly in the workgroup (one set, one chunk)
+    constexpr bool ZI = FLAGS & kZeroI, ZF = FLAGS & kZeroF;  // zero-twiddle top layers
     static_assert(!(SCALE && MULTI_IN) && !(REVEAL && MULTI_OUT), "unsupported combination");
+    static_assert(!(ZI && MULTI_IN) && !(ZF && MULTI_OUT), "zero-twiddle layers: one chunk per transform");
     static_assert(!EVAL || (SCALE && K <= 6), "fused eval_poly: single-pass decodes of <= 64 rows");
     constexpr int PL = P::NPH - 1;  // phase after an IFFT / before an FFT
     uint32_t *plane = lds;
@@ -833,7 +853,7 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
     if constexpr (SCALE) scale_rows<K, LR, SPL, 0>(c, tabS, lo, hi);
 
     if constexpr (DO_IFFT) {
-        transform<K, LR, SPL, true>(c, plane, tabI, lo, hi);
+        transform<K, LR, SPL, true, ZI>(c, plane, tabI, lo, hi);
         if constexpr (MULTI_IN) {
             for (uint32_t ci = 1; ci < A.in_chunks; ++ci) {
                 const uint32_t chunk = gchunk + ci;
@@ -861,7 +881,7 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
     if constexpr (XOR_IN) static_for<0, P::R>([&](auto ic) { lo[ic] ^= xl[ic]; hi[ic] ^= xh[ic]; });
 
     if constexpr (DO_FFT && !MULTI_OUT) {
-        transform<K, LR, SPL, false>(c, plane, tabF, lo, hi);
+        transform<K, LR, SPL, false, ZF>(c, plane, tabF, lo, hi);
         store_rows<K, LR, SPL, 0, REVEAL>(A, c, gchunk, tabV, rinfo, lo, hi);
     } else if constexpr (DO_FFT) {
         for (uint32_t co = 0; co < A.out_chunks; ++co) {
@@ -884,7 +904,9 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
 // SIMD (<= 80 VGPRs) so that three of its workgroups share a CU: one's row
 // loads and stores overlap the others' layers.
 template <int LR, int FLAGS>
-constexpr int pass_waves_per_eu() { return FLAGS == (kIfft | kFft) && LR == 3 ? 6 : 2; }
+constexpr int pass_waves_per_eu() {
+    return (FLAGS & ~(kZeroI | kZeroF)) == (kIfft | kFft) && LR == 3 ? 6 : 2;
+}
 
 template <int K, int LR, int SPL, int FLAGS>
 __global__ void __launch_bounds__(1 << (K - LR + SPL), (pass_waves_per_eu<LR, FLAGS>())) k_pass(const PassArgs A) {
@@ -924,6 +946,16 @@ hipError_t launch_k(int flags, const PassArgs &A, hipStream_t s) {
         flags |= kEval;
     }
     constexpr int I = kIfft, F = kFft;
+    // zero-twiddle top layers (RS_MONO_ZERO_TOP): the pass holds the transform's top
+    // bit (a + K = log2 n) and every chunk of the launch has skew offset 0; the
+    // fused top passes of encodes (FFT) and decodes (both) have variants for it
+    if (RS_MONO_ZERO_TOP && K > 0 && A.n > 1 && A.a + uint32_t(K) == uint32_t(__builtin_ctz(A.n))) {
+        const bool one = A.grid_chunks == 1;
+        const bool zi = (flags & I) && A.ifft_delta == 0 && A.in_chunks == 1 && (one || A.ifft_delta_step == 0);
+        const bool zf = (flags & F) && A.fft_delta == 0 && A.out_chunks == 1 && (one || A.fft_delta_step == 0);
+        if (flags == (I | F) && zf && !zi) return launch_f<K, LR, SPL, I | F | kZeroF>(A, s);
+        if (flags == (I | F | kFd) && zi && zf) return launch_f<K, LR, SPL, I | F | kFd | kZeroI | kZeroF>(A, s);
+    }
     switch (flags) {
         // encode / engine
         case I: return launch_f<K, LR, SPL, I>(A, s);
