@@ -948,12 +948,16 @@ hipError_t launch_k(int flags, const PassArgs &A, hipStream_t s) {
     constexpr int I = kIfft, F = kFft;
     // zero-twiddle top layers (RS_MONO_ZERO_TOP): the pass holds the transform's top
     // bit (a + K = log2 n) and every chunk of the launch has skew offset 0; the
-    // fused top passes of encodes (FFT) and decodes (both) have variants for it
+    // fused top passes of encodes (HighRate: FFT; LowRate: IFFT) and decodes (both)
+    // have variants for it
     if (RS_MONO_ZERO_TOP && K > 0 && A.n > 1 && A.a + uint32_t(K) == uint32_t(__builtin_ctz(A.n))) {
         const bool one = A.grid_chunks == 1;
         const bool zi = (flags & I) && A.ifft_delta == 0 && A.in_chunks == 1 && (one || A.ifft_delta_step == 0);
         const bool zf = (flags & F) && A.fft_delta == 0 && A.out_chunks == 1 && (one || A.fft_delta_step == 0);
         if (flags == (I | F) && zf && !zi) return launch_f<K, LR, SPL, I | F | kZeroF>(A, s);
+        // LowRate: the IFFT of the originals at skew offset 0, FFTs at c n + n
+        if (flags == (I | F) && zi && !zf) return launch_f<K, LR, SPL, I | F | kZeroI>(A, s);
+        if (flags == (I | F | kMultiOut) && zi) return launch_f<K, LR, SPL, I | F | kMultiOut | kZeroI>(A, s);
         if (flags == (I | F | kFd) && zi && zf) return launch_f<K, LR, SPL, I | F | kFd | kZeroI | kZeroF>(A, s);
     }
     switch (flags) {
