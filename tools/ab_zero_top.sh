@@ -8,7 +8,7 @@ source tools/ab_common.sh
 OUT=gpurun_out/ab_zero_top
 mkdir -p $OUT
 for r in 1 2; do
-  for v in zt0 main; do
+  for v in ${VARIANT:-zt0} main; do
     use_lib $v
     timeout -k 10 240 python -u tools/route_time.py ${SHAPES:-8192:8192:65536 32768:32768:65536} --iters 5 > $OUT/${v}_$r.jsonl
   done
