@@ -20,7 +20,11 @@ of every shard), an RCCL all-gather of the recovery slices over xGMI and a
 re-interleave -- total work fixed, strong scaling -- with its encode-only time,
 the all-gather cost, the per-GPU HBM fraction and a column-partitioned 1 % decode;
 its N = 1 point is in the --gpus 1 line.  --config 32768x32768x64k makes that
-workload the primary line instead (strong scaling).
+workload the primary line instead (strong scaling).  The other single-GPU
+BASELINE configs ride in the same line: "config3" = configs[2] (32768:32768 x
+1 KiB encode, plus its 1 % / 100 % decode) and "config4" = configs[3]
+(8192:8192 x 64 KiB decode at 1 % / 100 %), each with the roofline of its
+dominant kernel (replicas per rank at N > 1; --no-configs skips them).
 
 Timing: W untimed warmup steps, then exactly K steps bracketed by a barrier +
 torch.cuda.synchronize() on both sides, max over ranks.  Nothing else runs in
@@ -81,6 +85,8 @@ def parse():
     p.add_argument("--no-object", action="store_true", help="skip the object-API (encoder/decoder) measurement")
     p.add_argument("--no-sharded", action="store_true",
                    help="skip the configs[4] strong-scaling sub-object (column partition + all-gather)")
+    p.add_argument("--no-configs", action="store_true",
+                   help="skip the configs[2] / configs[3] sub-objects of the headline line")
     p.add_argument("--profile-steps", type=int, default=50)
     p.add_argument("--batch", type=int, default=64, help="stripes per call of the batched measurement (1 = skip)")
     p.add_argument("--plumbing", action="store_true",
@@ -275,7 +281,9 @@ def roofline_of(rs, ctx, fn, profile_steps, alg_step_bytes, config, launch_scope
         a[0] += ms
         a[1] += 1
         a[2] += by
-    kernels = {k: {"launches_per_step": v[1] / profile_steps, "avg_us": round(1e3 * v[0] / v[1], 3),
+    # per-launch event figures: each launch bracketed by its own pair of events, which adds
+    # the events' own gaps (≈2.6 µs on the 8 µs headline launch) -- NOT the roofline's avg_us
+    kernels = {k: {"launches_per_step": v[1] / profile_steps, "event_bracketed_us": round(1e3 * v[0] / v[1], 3),
                    "alg_bytes_per_launch": v[2] // v[1]} for k, v in agg.items()}
     dom = max(agg, key=lambda k: agg[k][0])
     kernel_s_per_step = sum(v[0] for v in agg.values()) / 1e3 / profile_steps
@@ -304,8 +312,60 @@ def roofline_of(rs, ctx, fn, profile_steps, alg_step_bytes, config, launch_scope
             "algorithmic_bytes": alg_step_bytes, "avg_us": round(dom_avg_s * 1e6, 3),
             "valu_frac": valu["frac"] if valu else None, "valu": valu, "kernels": kernels,
             "note": "scope 'launch': one launch is the whole step, avg_us = launch-stream event time of a whole "
-                    "batch / steps (rocprofv3 kernel-trace average agrees, profiles/); otherwise achieved = the "
-                    "step's algorithmic bytes / the summed durations of the step's launches"}
+                    "batch / steps (rocprofv3 kernel-trace average agrees, profiles/); otherwise avg_us = the "
+                    "dominant kernel's event-bracketed launch time and achieved = the step's algorithmic bytes / "
+                    "the summed durations of the step's launches. kernels[*].event_bracketed_us: every launch "
+                    "between its own events (includes the events' gaps)"}
+
+
+def compact_roofline(rl):
+    return {k: rl[k] for k in ("kernel", "achieved", "frac", "avg_us", "traffic", "valu_frac", "algorithmic_bytes")}
+
+
+def config_block(args, rs, ctx, name, world, dev, encode=True, decode=True):
+    """One more single-GPU BASELINE config in the headline line (configs[2], configs[3]): the
+    same device-resident calls, timed the same way (W untimed, K timed between barrier +
+    synchronize, max over ranks; every rank an independent stripe), with the roofline of the
+    dominant kernel of each operation.  Decode: the reference's loss pattern
+    (benches/benchmarks.rs:113-138) at 1 % and 100 %; algorithmic bytes = received + restored rows."""
+    import torch
+
+    N, M, S = CONFIGS[name]
+    timed, gpu_time = make_timer(world, dev)
+    steps, warm = (max(3, min(args.steps, 20)), 3) if N * S <= (64 << 20) else (max(3, min(args.steps, 10)), 2)
+    g = torch.Generator(device=dev)
+    g.manual_seed(99 + N + S)
+    d_orig = torch.randint(0, 256, (N, S), dtype=torch.uint8, device=dev, generator=g)
+    d_rec = torch.empty((M, S), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.Stream(device=dev)
+    enc = rs.encode_device_call(N, M, S, d_orig, d_rec, stream=stream, ctx=ctx)
+    step_bytes = (N + M) * S
+    out = {"workload": f"{N}:{M} x {S} B", "steps": steps, "parallelism": f"replicas x{world}"}
+    if encode:
+        w = timed(enc, steps, warm)
+        gt = gpu_time(enc, steps, stream)
+        out["encode"] = {"GiBps": round(step_bytes * steps * world / w / 2**30, 2),
+                         "us_per_step": round(w / steps * 1e6, 1),
+                         "roofline": compact_roofline(roofline_of(rs, ctx, enc, 3, step_bytes, name, gt / steps))}
+    else:
+        enc()
+    if decode:
+        d_out = torch.empty((N, S), dtype=torch.uint8, device=dev)
+        for pct in (1, 100):
+            L = -(-min(N, M) * pct // 100)
+            op = rs.present_mask([1] * (N - L) + [0] * L)
+            rp = rs.present_mask([1] * L + [0] * (M - L))
+            dec = rs.decode_device_call(N, M, S, d_orig, op, d_rec, rp, d_out, stream=stream, ctx=ctx)
+            w = timed(dec, steps, warm)
+            gt = gpu_time(dec, steps, stream)
+            out[f"decode_{pct}pct"] = {
+                "GiBps": round(step_bytes * steps * world / w / 2**30, 2), "us_per_step": round(w / steps * 1e6, 1),
+                "roofline": compact_roofline(roofline_of(rs, ctx, dec, 3, (N + L) * S, name, gt / steps))}
+        del d_out
+    stream.synchronize()
+    del d_orig, d_rec
+    torch.cuda.empty_cache()
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -430,6 +490,12 @@ def stripe_bench(args, rs, ctx, config, world, rank, dev):
 
     copy_ref = None if args.no_copy else device_copy(dev)
 
+    # ---- the other single-GPU BASELINE configs, in the same line ----------------
+    cfg3 = cfg4 = None
+    if config == HEADLINE and not args.no_configs:
+        cfg3 = config_block(args, rs, ctx, "32768x32768x1k", world, dev)                 # configs[2]
+        cfg4 = config_block(args, rs, ctx, "8192x8192x64k", world, dev, encode=False)    # configs[3]
+
     # ---- configs[4] at the same N: strong scaling, column partition + RCCL all-gather ----
     sharded = None
     if config == HEADLINE and not args.no_sharded:
@@ -443,8 +509,9 @@ def stripe_bench(args, rs, ctx, config, world, rank, dev):
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 5), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (uniform random bytes)",
+            "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 6),
+            "us_per_step": round(wall / args.steps * 1e6, 2), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic (uniform random bytes)",
             "config": {"workload": f"encode {N}:{M} x {S} B, device-resident (rs_encode_device)",
                        "original_count": N, "recovery_count": M, "shard_bytes": S,
                        "rate": "high" if rs.use_high_rate(N, M) == 1 else "low",
@@ -455,9 +522,12 @@ def stripe_bench(args, rs, ctx, config, world, rank, dev):
             "host_e2e": host_e2e,
             "object_api": object_api,
             "roofline": roofline,
-            "sharded": sharded,
-            "device_copy": copy_ref,
             "cpu_baseline": cpu,
+            "device_copy": copy_ref,
+            # last, so that a reader of the line's tail sees configs[2..4]
+            "sharded": sharded,
+            "config3": cfg3,
+            "config4": cfg4,
         }
         print(json.dumps(line))
 

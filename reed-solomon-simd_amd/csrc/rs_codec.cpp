@@ -210,7 +210,7 @@ struct rs_context {
     // profiles/r05c): 256:256 x 1 KiB 4.72 -> 4.35 us, 512:512 5.61 -> 5.50 us, but
     // 1024:1024 8.09 -> 8.70 us (its layers' exchange chain is longer than k_mono's)
     bool lane = true, lane_default = true;
-    int lane_max_l = 9;
+    int lane_max_l = 9, lane_max_l_default = 9;
     // half-split 2^12-row transforms (half_split below; RS_MI355X_HALF=0/1;
     // rs_mono_enable + 128: on, + 256: off).  Off by default: measured slower than
     // the pass kernels at every shape tried (4096:4096 x 1 KiB encode 19.5 -> 25.0 us,
@@ -222,6 +222,7 @@ struct rs_context {
     // RS_MI355X_CHUNKS=0/1; rs_mono_enable + 512: on, + 1024: off)
     bool chunks = true, chunks_default = true;
     bool chunks_forced = false;  // every multi-chunk shape k_chunks supports (+ 512)
+    bool chunks_forced_default = false;  // RS_MI355X_CHUNKS=2 at context creation
     uint32_t *d_top = nullptr;    // layer-11 perm tables of the half-split kernels (top_table)
     bool pad_small = true;        // decodes of 16..64 work rows on the 2^7-row column kernel (RS_MI355X_PAD_SMALL)
     int chunk_par = -1;           // RS_MI355X_CHUNK_PARALLEL: -1 by pack count (chunk_parallel), 0 / 1 forced
@@ -1560,6 +1561,7 @@ rs_status rs_context_create(int device, rs_context **out) {
             ctx->chunks_forced = ck[0] == '2';
         }
         ctx->chunks_default = ctx->chunks;
+        ctx->chunks_forced_default = ctx->chunks_forced;
         {  // top_table: skew index 2047 + 2048 j, both table formats
             std::vector<uint32_t> top(size_t(kTopTables) * (rs::kPermWords + rs::kPerm2Words));
             for (uint32_t j = 0; j < kTopTables; ++j) {
@@ -1758,7 +1760,11 @@ uint64_t slice_width(uint64_t S, uint32_t slices) {
 // `span_ok` (the destination's other rows are scratch nobody reads), more than
 // kCopyRuns runs go as one copy of the span from the first to the last wanted row:
 // every copy costs ~10 us of latency, so scattered losses (hundreds of runs) would
-// otherwise cost more than the bytes they skip.
+// otherwise cost more than the bytes they skip.  Span copies carry absent rows in and
+// present rows out, so they rely on two invariants: no decode route reads an absent
+// row of d_orig / d_rec (erased rows load as zero, decode_dev), and only missing rows
+// of an output staging are read back (restored_original); pinned by
+// tests/test_gpu_parity.py::test_decode_ignores_absent_rows_and_stale_staging.
 constexpr uint64_t kCopyRuns = 4;
 void copy_rows(uint8_t *dst, const uint8_t *src, uint64_t pitch, uint64_t width, const uint8_t *flag, uint8_t want,
                uint64_t rows, hipMemcpyKind kind, hipStream_t s, bool span_ok = false) {
@@ -2468,12 +2474,13 @@ rs_status rs_mono_enable(rs_context *ctx, int enable) {
     ctx->e2_encode = !(enable & 8);
     // + 32: lane kernel on, + 64: off (neither: the context's default)
     ctx->lane = (enable & 32) ? true : (enable & 64) ? false : ctx->lane_default;
-    ctx->lane_max_l = (enable & 32) ? 10 : 9;
+    ctx->lane_max_l = (enable & 32) ? 10 : ctx->lane_max_l_default;
     // + 128: half-split 2^12-row transforms on, + 256: off
     ctx->half = (enable & 128) ? true : (enable & 256) ? false : ctx->half_default;
     // + 512: multi-chunk kernel on, + 1024: off
     ctx->chunks = (enable & 512) ? true : (enable & 1024) ? false : ctx->chunks_default;
-    ctx->chunks_forced = (enable & 512) != 0;
+    // (neither bit: the context's defaults, RS_MI355X_CHUNKS=2's forced routing included)
+    ctx->chunks_forced = (enable & 512) ? true : (enable & 1024) ? false : ctx->chunks_forced_default;
     return RS_OK;
 }
 

@@ -1770,6 +1770,18 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 else
                     write1();
             }
+#ifdef RS_MONO_HALF_RACE_PROBE
+            // tools/half_race_demo.sh: poison the shared region, then hold back every
+            // wave but wave 0 before it writes its shared pieces -- a reader that does
+            // not wait for the region's writers sees the poison, deterministically
+            if constexpr (HALF_F) {
+                for (uint32_t q = threadIdx.x; q < kSh * G::SW / 4; q += T)
+                    reinterpret_cast<uint4 *>(shared)[q] = uint4{0xEEEEEEEEu, 0xEEEEEEEEu, 0xEEEEEEEEu, 0xEEEEEEEEu};
+                __syncthreads();
+                if (wave != 0)
+                    for (int k = 0; k < 8; ++k) __builtin_amdgcn_s_sleep(127);
+            }
+#endif
             static_for<0, KSH>([&](auto kc) {
                 const uint32_t q = threadIdx.x + T * decltype(kc)::value;
                 if (q < LPC * kSh) G::put(shared, q, vs[kc], [](uint32_t p) { return G::atS(p); });
@@ -1912,6 +1924,19 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                     else fft_bfly(c.lo[i], c.hi[i], cb.lo[i], cb.hi[i], tf);
                 });
                 if (hh & 1u) c = cb;
+                // The FFT's first layers (phase 4) read the shared region, which every
+                // wave of the workgroup wrote above: wait for all of them.  The decode
+                // waits inside formal_derivative; the encode had no barrier between
+                // those writes and these reads, so a wave could read another wave's
+                // slots before they were written -- what LDS held before (often the
+                // same tables, left by the previous launch of this kernel on the CU;
+                // not on the first launch in a process) -- the round-5 parity failure
+                // of test_half_split_encode_matches_oracle[high-1-2049-64-129]
+                // (profiles/r05j/pytest_gpu_multiin_fail.log; r06 demonstration:
+                // tools/half_race_demo.sh, profiles/r06a/half_race_demo.txt)
+#ifndef RS_MONO_NO_HALF_BARRIER
+                if constexpr (!HFD) __syncthreads();
+#endif
                 RS_MSTAMP(6);
                 using SF = SeqOf<L, LR, true, PK>;
                 constexpr int NLF = num_layers(SF::v);

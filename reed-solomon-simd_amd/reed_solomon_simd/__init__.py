@@ -1088,23 +1088,50 @@ class ShardedDecoder(_ColumnSplit):
         super().__init__(original_count, recovery_count, shard_bytes, device, group, stream, rate_, ctx, chunks,
                          force_collective)
         self._decode_slice = decode_slice
-        self.part = (torch.empty((original_count, self.w), dtype=torch.uint8, device=self.dev)
-                     if self.collective else None)
-        self._pattern = None  # (original mask, missing-row index, packed pieces, gathered pieces)
+        N, dev = original_count, self.dev
+        self.part = torch.empty((N, self.w), dtype=torch.uint8, device=dev) if self.collective else None
+        # packed / gathered restored rows of each piece, allocated once for the most rows a
+        # pattern can restore (N) and narrowed per pattern: a loss pattern that changes from
+        # stripe to stripe costs no allocation
+        self._packed = [torch.empty(N * self.cw, dtype=torch.uint8, device=dev) for _ in range(self.chunks)] \
+            if self.collective else []
+        self._gathered = [torch.empty(self.world * N * self.cw, dtype=torch.uint8, device=dev)
+                          for _ in range(self.chunks)] if self.collective else []
+        self._pattern = None  # (original mask, missing-row index, its host copy, packed, gathered)
+        self._check_masks = os.environ.get("RS_MI355X_DEBUG_MASKS") == "1"
+
+    def _same_on_every_rank(self, op: bytes) -> None:
+        """Debug (RS_MI355X_DEBUG_MASKS=1): every rank must pass the same erasure pattern --
+        the gathers are sized by its loss count, so ranks that differ would hang in them."""
+        import hashlib
+        import torch
+        import torch.distributed as dist
+
+        h = int.from_bytes(hashlib.sha256(op).digest()[:7], "little")
+        t = torch.tensor([h, -h], dtype=torch.int64, device=self.dev if self.nccl else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        if int(t[0]) != h or -int(t[1]) != h:
+            raise ValueError("ShardedDecoder: the ranks passed different original_present masks")
 
     def _prepare(self, op: bytes):
-        """Missing-row index and gather buffers of one erasure pattern (kept while it repeats)."""
+        """Missing-row index and gather views of one erasure pattern (kept while it repeats)."""
         if self._pattern is not None and self._pattern[0] == op:
             return self._pattern
         import numpy as np
         import torch
 
+        if self._check_masks:
+            self._same_on_every_rank(op)
         miss = np.flatnonzero(np.frombuffer(op, dtype=np.uint8) == 0).astype(np.int64)
         L, dev = len(miss), self.dev
-        idx = torch.from_numpy(miss).to(dev)
-        packed = [torch.empty((L, self.cw), dtype=torch.uint8, device=dev) for _ in range(self.chunks)]
-        gathered = [torch.empty((self.world, L, self.cw), dtype=torch.uint8, device=dev) for _ in range(self.chunks)]
-        self._pattern = (op, idx, packed, gathered)
+        host = torch.from_numpy(miss)
+        if dev.type == "cuda":  # pinned, so the index goes up without blocking the host
+            host = host.pin_memory()
+        idx = host.to(dev, non_blocking=True)
+        cw, world = self.cw, self.world
+        packed = [b[:L * cw].view(L, cw) for b in self._packed]
+        gathered = [b[:world * L * cw].view(world, L, cw) for b in self._gathered]
+        self._pattern = (op, idx, host, packed, gathered)
         return self._pattern
 
     def _decode(self, orig_cols, op, rec_cols, rp, out) -> None:
@@ -1125,7 +1152,7 @@ class ShardedDecoder(_ColumnSplit):
         if not self.collective:
             self._decode(orig_cols, op, rec_cols, rp, d_restored)
             return
-        _, idx, packed, gathered = self._prepare(op)
+        _, idx, _, packed, gathered = self._prepare(op)
         if idx.numel() == 0:  # nothing to restore (decoder_work.rs:131-132); the call still validates
             self._decode(orig_cols[:, self._piece(0)], op, rec_cols[:, self._piece(0)], rp,
                          self.part[:, self._piece(0)])

@@ -257,3 +257,96 @@ def _worker_forced(rank, world, port, q):
 def test_forced_collective_world1():
     out = _spawn(_worker_forced, 1)
     assert out == {0: (True, True, [128] * 4)}
+
+
+def _worker_config5_geometry(rank, world, port, N, M, S, q):
+    """configs[4]'s split at world 8: S = 64 KiB over 8 ranks is an 8 KiB slice
+    per rank, coded in 4 pieces of 2 KiB -- the smallest piece the default chunking allows.
+    Encode through ShardedEncoder and the cached encode_device_sharded, decode at 1 % / 100 % /
+    scattered loss through ShardedDecoder, with only the per-piece device call replaced by the
+    oracle (/root/reference/src/engine/utils.rs:35-43: every op is column-wise)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "reed-solomon-simd_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    import reed_solomon_simd as rs
+    _init(rank, world, port)
+    enc_w, dec_w = [], []
+
+    def enc_piece(cols, out):
+        enc_w.append(cols.shape[1])
+        out.copy_(torch.from_numpy(O.encode("high", np.ascontiguousarray(cols.numpy()), M)))
+
+    def dec_piece(orig_cols, op, rec_cols, rp, out):
+        dec_w.append(out.shape[1])
+        opa, rpa = np.frombuffer(op, np.uint8), np.frombuffer(rp, np.uint8)
+        got = O.decode("high", np.ascontiguousarray(orig_cols.numpy()), opa, np.ascontiguousarray(rec_cols.numpy()),
+                       rpa)
+        miss = np.flatnonzero(opa == 0)
+        out[torch.from_numpy(miss)] = torch.from_numpy(got[miss])
+
+    try:
+        orig = O.generate_original(N, S, 77)
+        want = O.encode("high", orig, M)
+        enc = rs.ShardedEncoder(N, M, S, rate_=1, encode_slice=enc_piece)
+        ok = {"encode": True, "decode": True}
+        d_rec = torch.zeros((M, S), dtype=torch.uint8)
+        enc(enc.columns(torch.from_numpy(orig)), d_rec)
+        ok["encode"] = bool(np.array_equal(d_rec.numpy(), want))
+        # the module-level entry point (cached ShardedEncoder) with the device call replaced
+        rs.encode_device = lambda n, m, w, cols, out, stream=None, rate_=0, ctx=None: enc_piece(cols, out)
+        d2 = torch.zeros((M, S), dtype=torch.uint8)
+        rs.encode_device_sharded(N, M, S, torch.from_numpy(orig), d2, rate_=1)
+        ok["encode"] = ok["encode"] and bool(np.array_equal(d2.numpy(), want))
+        rng = np.random.default_rng(123)
+        L1 = -(-min(N, M) // 100)
+        scat = np.ones(N, np.uint8)
+        scat[rng.choice(N, size=min(N, M) // 2, replace=False)] = 0
+        patterns = [([1] * (N - L1) + [0] * L1, [1] * L1 + [0] * (M - L1)),  # benchmarks.rs:113-138, 1 %
+                    ([0] * min(N, M) + [1] * (N - min(N, M)), [1] * M),       # 100 % (of min(N, M))
+                    (list(scat), [1] * M)]                                    # scattered
+        dec = rs.ShardedDecoder(N, M, S, rate_=1, decode_slice=dec_piece)
+        for op, rp in patterns + patterns[:1]:  # a repeat reuses the pattern's views
+            out = torch.full((N, S), 0xAB, dtype=torch.uint8)
+            dec(dec.columns(torch.from_numpy(orig)), op, dec.columns(torch.from_numpy(want)), rp, out)
+            o = out.numpy()
+            miss = np.flatnonzero(np.asarray(op) == 0)
+            keep = np.flatnonzero(np.asarray(op) != 0)
+            ok["decode"] = ok["decode"] and bool(np.array_equal(o[miss], orig[miss])) and bool((o[keep] == 0xAB).all())
+        q.put((rank, (ok, enc.w, enc.chunks, sorted(set(enc_w)), sorted(set(dec_w)))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world8_config5_geometry():
+    """World 8 at configs[4]'s column geometry (64 KiB shards: 8 KiB per rank, 4 pieces of
+    2 KiB), with few rows so the oracle finishes in seconds."""
+    N, M, S = 200, 100, 65536
+    out = _spawn(_worker_config5_geometry, 8, N, M, S)
+    assert out == {r: ({"encode": True, "decode": True}, 8192, 4, [2048], [2048]) for r in range(8)}, out
+
+
+def _worker_mask_mismatch(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "reed-solomon-simd_amd"))
+    import reed_solomon_simd as rs
+    _init(rank, world, port)
+    try:
+        os.environ["RS_MI355X_DEBUG_MASKS"] = "1"
+        dec = rs.ShardedDecoder(64, 64, 256, rate_=1, decode_slice=lambda *a: None)
+        op = [1] * 64
+        op[rank] = 0  # a different lost shard on every rank
+        try:
+            dec(torch.zeros((64, 128), dtype=torch.uint8), op, torch.zeros((64, 128), dtype=torch.uint8), [1] * 64,
+                torch.zeros((64, 256), dtype=torch.uint8))
+            q.put((rank, "no error"))
+        except ValueError as e:
+            q.put((rank, "different" in str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_decoder_rejects_different_masks_in_debug_mode():
+    """the gathers are sized by the loss count, so ranks with different erasure
+    patterns would hang; RS_MI355X_DEBUG_MASKS=1 all-reduces a hash of the mask first."""
+    assert _spawn(_worker_mask_mismatch, 2) == {0: True, 1: True}

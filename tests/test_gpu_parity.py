@@ -40,6 +40,27 @@ def _dev(torch, a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
+def assert_rows_equal(got, want, what="rows"):
+    """Byte-exact comparison that names the first differing (row, byte), the number of
+    differing bytes and rows, and the first differing rows' indices -- enough to tell a
+    whole-table race (many rows of one column) from a single corrupted row."""
+    got = np.asarray(got)
+    want = np.asarray(want)
+    assert got.shape == want.shape, f"{what}: shape {got.shape} != {want.shape}"
+    diff = got != want
+    if not diff.any():
+        return
+    rows = np.flatnonzero(diff.reshape(diff.shape[0], -1).any(axis=1))
+    r0 = int(rows[0])
+    b0 = int(np.flatnonzero(diff[r0].reshape(-1))[0])
+    cols = np.flatnonzero(diff.reshape(diff.shape[0], -1).any(axis=0))
+    raise AssertionError(
+        f"{what}: {int(diff.sum())} of {diff.size} bytes differ in {rows.size} of {diff.shape[0]} rows; "
+        f"first at (row {r0}, byte {b0}): got {int(got.reshape(got.shape[0], -1)[r0, b0])} want "
+        f"{int(want.reshape(want.shape[0], -1)[r0, b0])}; rows {rows[:16].tolist()}; byte columns {cols[:16].tolist()}"
+        f"{' ...' if cols.size > 16 else ''}")
+
+
 def gpu_encode(torch, rs, rate, orig, M):
     N, S = orig.shape
     d_orig = _dev(torch, orig)
@@ -80,7 +101,7 @@ def test_encode_device_matches_oracle(torch, rs, rate, N, M, S):
     orig = O.generate_original(N, S, (N * 31 + M) & 0xFF)
     want = O.encode(rate, orig, M)
     got = gpu_encode(torch, rs, rate, orig, M)
-    assert np.array_equal(got, want)
+    assert_rows_equal(got, want)
 
 
 # Single-level multi-chunk encodes in both forms (rs_codec.cpp chunk_parallel): chunks one
@@ -104,7 +125,7 @@ def test_chunk_forms_match_oracle(torch, rs, forced, monkeypatch):
             d_rec = torch.full((M, S), 0xEE, dtype=torch.uint8, device="cuda")
             rs.encode_device(N, M, S, d_orig, d_rec, rate_=RATE[rate], ctx=ctx)
             torch.cuda.synchronize()
-            assert np.array_equal(d_rec.cpu().numpy(), want), (forced, rate, N, M, S)
+            assert_rows_equal(d_rec.cpu().numpy(), want, str((forced, rate, N, M, S)))
     finally:
         ctx.close()
 
@@ -131,8 +152,8 @@ def test_decode_device_matches_oracle(torch, rs, rate, N, M, S, loss):
     want = O.decode(rate, orig, op, rec, rp)
     got = gpu_decode(torch, rs, rate, orig, op, rec, rp)
     miss = op == 0
-    assert np.array_equal(got[miss], orig[miss])
-    assert np.array_equal(got[miss], want[miss])
+    assert_rows_equal(got[miss], orig[miss])
+    assert_rows_equal(got[miss], want[miss])
     assert np.all(got[~miss] == 0x33), "present rows of the output must not be written"
 
 
@@ -468,7 +489,7 @@ def test_engine_transforms(torch, rs, size, pos, delta, trunc, blocks, which):
     getattr(rs.engine, which)(d, rows, blocks, pos, size, trunc, delta)
     torch.cuda.synchronize()
     got = d.cpu().numpy()
-    assert np.array_equal(got, want)
+    assert_rows_equal(got, want)
 
 
 def test_engine_mul_and_formal_derivative(torch, rs):
@@ -480,7 +501,7 @@ def test_engine_mul_and_formal_derivative(torch, rs):
         d = _dev(torch, x)
         rs.engine.mul(d, 10, lm)
         torch.cuda.synchronize()
-        assert np.array_equal(d.cpu().numpy(), want)
+        assert_rows_equal(d.cpu().numpy(), want)
     # utils.rs:99-104 is defined for power-of-two row counts only (it slices past
     # the end otherwise); the device API rejects other counts
     for n in (1, 2, 64, 1024):
@@ -490,7 +511,7 @@ def test_engine_mul_and_formal_derivative(torch, rs):
         d = _dev(torch, x)
         rs.engine.formal_derivative(d, n, 1)
         torch.cuda.synchronize()
-        assert np.array_equal(d.cpu().numpy(), want)
+        assert_rows_equal(d.cpu().numpy(), want)
     with pytest.raises(ValueError):
         rs.engine.formal_derivative(_dev(torch, np.zeros((3, 64), np.uint8)), 3, 1)
 
@@ -507,14 +528,14 @@ def test_engine_host_slices_match_oracle(torch, rs, which):
         getattr(O.lib(), f"orc_{which}")(O.ptr(want), blocks, pos, size, trunc, delta)
         got = x.copy()
         getattr(rs.engine, f"{which}_host")(got, rows, blocks, pos, size, trunc, delta)
-        assert np.array_equal(got, want), (size, pos, trunc, delta)
+        assert_rows_equal(got, want, str((size, pos, trunc, delta)))
     x = rng.integers(0, 256, (7, 64), dtype=np.uint8)
     for lm in (0, 12345, 65535):
         want = x.copy()
         O.lib().orc_mul(O.ptr(want), 7, lm)
         got = x.copy()
         rs.engine.mul_host(got, 7, lm)
-        assert np.array_equal(got, want)
+        assert_rows_equal(got, want)
 
 
 # ---------------------------------------------------------------------------
@@ -538,7 +559,7 @@ def test_stream_scratch_is_capped_and_released(torch, rs):
             rs.encode_device(N, M, S, d_o[(k + rep) & 1], outs[k], rate_=rs.RATE_HIGH, stream=st)
         torch.cuda.synchronize()
         for k, o in enumerate(outs):
-            assert np.array_equal(o.cpu().numpy(), wants[(k + rep) & 1]), (rep, k)
+            assert_rows_equal(o.cpu().numpy(), wants[(k + rep) & 1], str((rep, k)))
     for st in streams:
         rs.release_stream_scratch(st)
     rs.release_stream_scratch(streams[0])  # already released: no-op
@@ -598,7 +619,7 @@ def test_two_streams_share_one_context(torch, rs):
             rs.encode_device(N, M, S, d_o[k], d_r[k], stream=streams[k], rate_=RATE[rate])
     torch.cuda.synchronize()
     for k in range(2):
-        assert np.array_equal(d_r[k].cpu().numpy(), wants[k]), f"stream {k}"
+        assert_rows_equal(d_r[k].cpu().numpy(), wants[k], f"stream {k}")
     rng = np.random.default_rng(5)
     L = 1500
     op = np.ones(N, np.uint8)
@@ -613,7 +634,7 @@ def test_two_streams_share_one_context(torch, rs):
     torch.cuda.synchronize()
     miss = op == 0
     for k in range(2):
-        assert np.array_equal(outs[k].cpu().numpy()[miss], origs[k][miss]), f"stream {k}"
+        assert_rows_equal(outs[k].cpu().numpy()[miss], origs[k][miss], f"stream {k}")
 
 
 def test_device_arguments_are_checked(torch, rs):
@@ -644,7 +665,7 @@ def _column_sample_check(orig, got, M, rate, blocks=(0, 7, -1)):
         b %= nb
         cols = slice(64 * b, 64 * b + 64)
         want = O.encode(rate, np.ascontiguousarray(orig[:, cols]), M)
-        assert np.array_equal(got[:, cols], want), f"column block {b}"
+        assert_rows_equal(got[:, cols], want, f"column block {b}")
 
 
 @pytest.mark.parametrize("N,M,S", [(1024, 1024, 1024), (32768, 32768, 1024)])
@@ -655,7 +676,7 @@ def test_baseline_encode_configs(torch, rs, N, M, S):
     if N * S <= (64 << 20):
         O.lib().orc_select_engine(1)
         try:
-            assert np.array_equal(got, O.encode("default", orig, M))
+            assert_rows_equal(got, O.encode("default", orig, M))
         finally:
             O.lib().orc_select_engine(0)
 
@@ -674,7 +695,7 @@ def _sampled_blocks_match(torch, d_orig, d_rec, M, blocks):
     finally:
         O.lib().orc_select_engine(0)
     for k, b in enumerate(blocks):
-        assert np.array_equal(got[:, 64 * k:64 * k + 64], want[:, 64 * k:64 * k + 64]), f"column block {b}"
+        assert_rows_equal(got[:, 64 * k:64 * k + 64], want[:, 64 * k:64 * k + 64], f"column block {b}")
 
 
 def test_config5_full_size_encode(torch, rs):
@@ -767,7 +788,7 @@ def test_large_matrix_passes_match_oracle(torch, rs, rate, N, M, S, loss):
         want = O.encode(rate, o, M)
     finally:
         O.lib().orc_select_engine(0)
-    assert np.array_equal(got, want)
+    assert_rows_equal(got, want)
     rng = np.random.default_rng(N)
     L = max(1, int(min(N, M) * loss))
     op = np.ones(N, np.uint8)
@@ -800,7 +821,7 @@ def test_pass_path_matches_oracle(torch, rs, rate, N, M, S):
         orig = O.generate_original(N, S, (N + M + S) & 0xFF)
         want = O.encode(rate, orig, M)
         got = gpu_encode(torch, rs, rate, orig, M)
-        assert np.array_equal(got, want)
+        assert_rows_equal(got, want)
         rng = np.random.default_rng(N * 7 + M)
         L = min(N, M)
         op = np.ones(N, np.uint8)
@@ -827,7 +848,7 @@ def test_repeated_launches_stay_exact(torch, rs):
     for _ in range(200):
         rs.encode_device(N, M, S, d_orig, d_rec, rate_=1)
     rs.check_device()
-    assert np.array_equal(d_rec.cpu().numpy(), want)
+    assert_rows_equal(d_rec.cpu().numpy(), want)
 
 
 # ---------------------------------------------------------------------------
@@ -844,7 +865,7 @@ def test_strided_column_slice_encode_decode(torch, rs, rate, N, M, S, cols):
     rs.encode_device(N, M, b - a, d_orig[:, a:b], d_rec[:, a:b], rate_=RATE[rate])
     torch.cuda.synchronize()
     got = d_rec.cpu().numpy()
-    assert np.array_equal(got[:, a:b], want[:, a:b])
+    assert_rows_equal(got[:, a:b], want[:, a:b])
     assert np.all(got[:, :a] == 0x77) and np.all(got[:, b:] == 0x77), "columns outside the slice untouched"
     rng = np.random.default_rng(1)
     L = min(N, M) // 2
@@ -859,7 +880,7 @@ def test_strided_column_slice_encode_decode(torch, rs, rate, N, M, S, cols):
     torch.cuda.synchronize()
     out = d_out.cpu().numpy()
     miss = op == 0
-    assert np.array_equal(out[miss][:, a:b], orig[miss][:, a:b])
+    assert_rows_equal(out[miss][:, a:b], orig[miss][:, a:b])
     assert np.all(out[:, :a] == 0x33) and np.all(out[:, b:] == 0x33)
 
 
@@ -886,7 +907,7 @@ def test_column_kernel_and_pass_paths_match_oracle(torch, rs, rate, N, M, S, mon
         orig = O.generate_original(N, S, (N * 3 + M + S) & 0xFF)
         want = O.encode(rate, orig, M)
         got = gpu_encode(torch, rs, rate, orig, M)
-        assert np.array_equal(got, want)
+        assert_rows_equal(got, want)
         rng = np.random.default_rng(N * 5 + M)
         for L in sorted({1, min(N, M) // 3 + 1, min(N, M)}):
             op = np.ones(N, np.uint8)
@@ -932,7 +953,7 @@ def test_lane_kernel_encode_matches_oracle(torch, rs, rate, N, M, S):
         d_r = torch.full((M, S), 0xEE, dtype=torch.uint8, device="cuda")
         route = _route_of(torch, rs, lambda: rs.encode_device(N, M, S, d_o, d_r, rate_=RATE[rate]))
         assert len(route) == 1 and route[0].startswith("k_lane<"), route
-        assert np.array_equal(d_r.cpu().numpy(), want)
+        assert_rows_equal(d_r.cpu().numpy(), want)
         # strided rows: column slices of wider matrices (the rows' base and stride differ)
         wo = torch.full((N, S + 64), 0x11, dtype=torch.uint8, device="cuda")
         wr = torch.full((M, S + 64), 0x22, dtype=torch.uint8, device="cuda")
@@ -940,7 +961,7 @@ def test_lane_kernel_encode_matches_oracle(torch, rs, rate, N, M, S):
         rs.encode_device(N, M, S, wo[:, 32:32 + S], wr[:, 32:32 + S], rate_=RATE[rate])
         torch.cuda.synchronize()
         got = wr.cpu().numpy()
-        assert np.array_equal(got[:, 32:32 + S], want)
+        assert_rows_equal(got[:, 32:32 + S], want)
         assert np.all(got[:, :32] == 0x22) and np.all(got[:, 32 + S:] == 0x22)
         # a batch of 3 stripes in one launch
         origs = [orig] + [O.generate_original(N, S, 90 + b) for b in range(2)]
@@ -949,7 +970,7 @@ def test_lane_kernel_encode_matches_oracle(torch, rs, rate, N, M, S):
         rs.encode_device_batch(N, M, S, b_o, b_r, rate_=RATE[rate])
         torch.cuda.synchronize()
         for b in range(3):
-            assert np.array_equal(b_r[b].cpu().numpy(), O.encode(rate, origs[b], M)), f"stripe {b}"
+            assert_rows_equal(b_r[b].cpu().numpy(), O.encode(rate, origs[b], M), f"stripe {b}")
     finally:
         rs.mono_enable(1)
 
@@ -982,7 +1003,7 @@ def test_chunks_kernel_encode_matches_oracle(torch, rs, rate, N, M, S, mono):
         d_r = torch.full((M, S), 0xEE, dtype=torch.uint8, device="cuda")
         route = _route_of(torch, rs, lambda: rs.encode_device(N, M, S, d_o, d_r, rate_=RATE[rate]))
         assert len(route) == 1 and route[0].startswith("k_chunks<"), route
-        assert np.array_equal(d_r.cpu().numpy(), want)
+        assert_rows_equal(d_r.cpu().numpy(), want)
         # strided rows: column slices of wider matrices
         wo = torch.full((N, S + 64), 0x11, dtype=torch.uint8, device="cuda")
         wr = torch.full((M, S + 64), 0x22, dtype=torch.uint8, device="cuda")
@@ -990,7 +1011,7 @@ def test_chunks_kernel_encode_matches_oracle(torch, rs, rate, N, M, S, mono):
         rs.encode_device(N, M, S, wo[:, 32:32 + S], wr[:, 32:32 + S], rate_=RATE[rate])
         torch.cuda.synchronize()
         got = wr.cpu().numpy()
-        assert np.array_equal(got[:, 32:32 + S], want)
+        assert_rows_equal(got[:, 32:32 + S], want)
         assert np.all(got[:, :32] == 0x22) and np.all(got[:, 32 + S:] == 0x22)
     finally:
         rs.mono_enable(1)
@@ -1052,7 +1073,7 @@ def test_half_split_encode_matches_oracle(torch, rs, rate, N, M, S, mono):
         d_r = torch.full((M, S), 0xEE, dtype=torch.uint8, device="cuda")
         route = _route_of(torch, rs, lambda: rs.encode_device(N, M, S, d_o, d_r, rate_=RATE[rate]))
         assert _half_modes(route, False) == [3, 5] and len(route) == 2, route
-        assert np.array_equal(d_r.cpu().numpy(), want)
+        assert_rows_equal(d_r.cpu().numpy(), want, "half-split encode")
         # strided rows: column slices of wider matrices
         wo = torch.full((N, S + 64), 0x11, dtype=torch.uint8, device="cuda")
         wr = torch.full((M, S + 64), 0x22, dtype=torch.uint8, device="cuda")
@@ -1060,7 +1081,7 @@ def test_half_split_encode_matches_oracle(torch, rs, rate, N, M, S, mono):
         rs.encode_device(N, M, S, wo[:, 32:32 + S], wr[:, 32:32 + S], rate_=RATE[rate])
         torch.cuda.synchronize()
         got = wr.cpu().numpy()
-        assert np.array_equal(got[:, 32:32 + S], want)
+        assert_rows_equal(got[:, 32:32 + S], want, "half-split encode, strided")
         assert np.all(got[:, :32] == 0x22) and np.all(got[:, 32 + S:] == 0x22)
     finally:
         rs.mono_enable(1)
@@ -1092,7 +1113,8 @@ def test_half_split_decode_matches_oracle(torch, rs, rate, N, M, S, kind, mono):
         assert _half_modes(route, True) == [4, 6] and len(route) == 3, route  # + k_eval_poly
         got = d_out.cpu().numpy()
         miss = op == 0
-        assert np.array_equal(got[miss], orig[miss]) and np.array_equal(got[miss], want[miss])
+        assert_rows_equal(got[miss], orig[miss], "half-split decode vs originals")
+        assert_rows_equal(got[miss], want[miss], "half-split decode vs oracle")
         assert np.all(got[~miss] == 0x33), "present rows of the output must not be written"
         rs.check_device()
     finally:
@@ -1136,7 +1158,7 @@ def test_host_pipeline_matches_oracle(torch, rs, rate, N, M, S, slices, pinned):
         h_o, h_r = orig.copy(), np.full((M, S), 0xEE, np.uint8)
     rs.encode_host(N, M, S, h_o, h_r, slices=slices, rate_=RATE[rate])
     got = h_r.numpy() if pinned else h_r
-    assert np.array_equal(got, want)
+    assert_rows_equal(got, want)
     rng = np.random.default_rng(N + M + S)
     L = max(1, min(N, M) // 3)
     op = np.ones(N, np.uint8)
@@ -1148,7 +1170,7 @@ def test_host_pipeline_matches_oracle(torch, rs, rate, N, M, S, slices, pinned):
                    np.where(rp[:, None] == 1, want, 0x5A).astype(np.uint8), rp, h_out, slices=slices,
                    rate_=RATE[rate])
     miss = op == 0
-    assert np.array_equal(h_out[miss], orig[miss])
+    assert_rows_equal(h_out[miss], orig[miss])
     assert np.all(h_out[~miss] == 0x33), "present rows of the output must not be written"
 
 
@@ -1176,7 +1198,7 @@ def test_batch_encode_decode_match_oracle(torch, rs, rate, N, M, S, B):
     got = d_r.cpu().numpy()
     recs = [O.encode(rate, origs[b], M) for b in range(B)]
     for b in range(B):
-        assert np.array_equal(got[b], recs[b]), f"stripe {b}"
+        assert_rows_equal(got[b], recs[b], f"stripe {b}")
     assert np.all(d_r_full[:, M:, :].cpu().numpy() == 0xEE), "padding rows must not be written"
     # one erasure pattern for every stripe
     rng = np.random.default_rng(N + M + B)
@@ -1193,7 +1215,7 @@ def test_batch_encode_decode_match_oracle(torch, rs, rate, N, M, S, B):
     out = d_out.cpu().numpy()
     miss = op == 0
     for b in range(B):
-        assert np.array_equal(out[b][miss], origs[b][miss]), f"stripe {b}"
+        assert_rows_equal(out[b][miss], origs[b][miss], f"stripe {b}")
         assert np.all(out[b][~miss] == 0x33)
 
 
@@ -1261,7 +1283,7 @@ def test_decode_loss_patterns_pruned_reveal(torch, rs, kind, rate, N, M, S, mono
         rp[np.random.default_rng(M).choice(M, L, replace=False)] = 1
         got = gpu_decode(torch, rs, rate, orig, op, rec, rp)
         miss = op == 0
-        assert np.array_equal(got[miss], orig[miss])
+        assert_rows_equal(got[miss], orig[miss])
         assert np.all(got[~miss] == 0x33), "present rows of the output must not be written"
         rs.check_device()
     finally:
@@ -1304,7 +1326,7 @@ def test_split_decode_matches_oracle(torch, rs, rate, N, M, S, kind):
             rs.mono_enable(1)
     miss = op == 0
     for got in outs:
-        assert np.array_equal(got[miss], orig[miss])
+        assert_rows_equal(got[miss], orig[miss])
         assert np.all(got[~miss] == 0x33), "present rows of the output must not be written"
     rs.check_device()
 
@@ -1320,7 +1342,7 @@ def test_bound_device_calls_match_oracle(torch, rs):
     for _ in range(3):
         enc()
     torch.cuda.synchronize()
-    assert np.array_equal(d_rec.cpu().numpy(), want)
+    assert_rows_equal(d_rec.cpu().numpy(), want)
     L = 11
     op = np.ones(N, np.uint8)
     op[N - L:] = 0
@@ -1366,7 +1388,7 @@ def _device_golden(torch, rs, c):
     torch.cuda.synchronize()
     out = d_out.cpu().numpy()
     miss = op == 0
-    assert np.array_equal(out[miss], orig[miss]), c["source"]
+    assert_rows_equal(out[miss], orig[miss], str(c["source"]))
     assert np.all(out[~miss] == 0x33)
 
 
@@ -1388,7 +1410,7 @@ def test_device_path_any_even_shard_size(torch, rs, rate, N, M, S):
     orig = O.generate_original(N, S, S)
     want = O.encode(rate, orig, M)
     got = gpu_encode(torch, rs, rate, orig, M)
-    assert np.array_equal(got, want)
+    assert_rows_equal(got, want)
     rng = np.random.default_rng(S + N)
     L = max(1, min(N, M) // 4)
     op = np.ones(N, np.uint8)
@@ -1397,7 +1419,7 @@ def test_device_path_any_even_shard_size(torch, rs, rate, N, M, S):
     rp[rng.choice(M, L, replace=False)] = 1
     out = gpu_decode(torch, rs, rate, orig, op, want, rp)
     miss = op == 0
-    assert np.array_equal(out[miss], orig[miss])
+    assert_rows_equal(out[miss], orig[miss])
     assert np.all(out[~miss] == 0x33)
 
 
@@ -1414,7 +1436,7 @@ def test_device_path_unaligned_matrices(torch, rs, rate, N, M, S, off, pad):
     rs.encode_device(N, M, S, d_ob[:, off:off + S], d_rb[:, off:off + S], rate_=RATE[rate])
     torch.cuda.synchronize()
     rb = d_rb.cpu().numpy()
-    assert np.array_equal(rb[:, off:off + S], want)
+    assert_rows_equal(rb[:, off:off + S], want)
     assert np.all(rb[:, :off] == 0xEE) and np.all(rb[:, off + S:] == 0xEE), "bytes around the slice must not change"
     rng = np.random.default_rng(N + S)
     L = max(1, min(N, M) // 3)
@@ -1428,7 +1450,7 @@ def test_device_path_unaligned_matrices(torch, rs, rate, N, M, S, off, pad):
     torch.cuda.synchronize()
     xb = d_xb.cpu().numpy()
     miss = op == 0
-    assert np.array_equal(xb[miss, off:off + S], orig[miss])
+    assert_rows_equal(xb[miss, off:off + S], orig[miss])
     assert np.all(xb[~miss] == 0x33)
     assert np.all(xb[:, :off] == 0x33) and np.all(xb[:, off + S:] == 0x33)
 
@@ -1443,7 +1465,7 @@ def test_batch_with_tail_shards(torch, rs, rate, N, M, S, B):
     torch.cuda.synchronize()
     got = d_r.cpu().numpy()
     for b in range(B):
-        assert np.array_equal(got[b], O.encode(rate, origs[b], M)), f"stripe {b}"
+        assert_rows_equal(got[b], O.encode(rate, origs[b], M), f"stripe {b}")
 
 
 def test_work_handoff_between_encoders_and_decoders(rs):
@@ -1487,3 +1509,61 @@ def test_work_handoff_between_encoders_and_decoders(rs):
         dec2.add_recovery_shard(i, rec[i].tobytes())
     restored = dict(dec2.decode().restored_original_iter())
     assert all(restored[i] == orig[i].tobytes() for i in range(100))
+
+
+# ---------------------------------------------------------------------------
+# copy_rows' span mode (rs_codec.cpp): with more than 4 runs of received rows, the host
+# pipeline and the decoder object copy whole spans, absent rows included, and the object's
+# D2H copy writes present rows of its output staging.  So every decode route must never
+# read an absent row of its inputs, and nothing may read present rows of the staging
+# (ADVICE r05).  Absent rows here hold another stripe's bytes (the object's staging left by
+# the previous decode) or 0xEE (the host pipeline's inputs), under scattered losses.
+
+SPAN_CASES = [
+    # (rate, N, M, S): the decode routes -- column kernel 2^11 (split / not), 2^7 padded,
+    # eval_poly + passes (2^12, 2^13 rows), one fused single pass, LowRate
+    ("high", 1024, 1024, 1024), ("high", 700, 300, 512), ("high", 40, 20, 320), ("high", 12, 4, 4096),
+    ("high", 2048, 2048, 256), ("high", 3000, 1000, 128), ("low", 100, 1000, 192), ("low", 300, 2500, 64),
+]
+
+
+@pytest.mark.parametrize("rate,N,M,S", SPAN_CASES)
+def test_decode_ignores_absent_rows_and_stale_staging(torch, rs, rate, N, M, S):
+    cls_d = {"high": rs.rate.HighRateDecoder, "low": rs.rate.LowRateDecoder}[rate]
+    rng = np.random.default_rng(N * 3 + M + S)
+    a = O.generate_original(N, S, 5)
+    b = O.generate_original(N, S, 6)
+    rec_a, rec_b = O.encode(rate, a, M), O.encode(rate, b, M)
+    L = max(1, min(N, M) // 2)
+    dec = cls_d(N, M, S)
+    # stripe a: lose a contiguous head, so the staging's rows of b's scattered losses hold a's bytes
+    op_a = np.ones(N, np.uint8)
+    op_a[:L] = 0
+    for i in np.flatnonzero(op_a):
+        dec.add_original_shard(int(i), a[i].tobytes())
+    for i in range(L):
+        dec.add_recovery_shard(i, rec_a[i].tobytes())
+    got = dict(dec.decode().restored_original_iter())
+    assert all(got[i] == a[i].tobytes() for i in range(L))
+    # stripe b: scattered losses (> 4 runs of received rows whenever L allows)
+    dec.reset(N, M, S)
+    op_b = np.ones(N, np.uint8)
+    op_b[rng.choice(N, L, replace=False)] = 0
+    rp_b = np.zeros(M, np.uint8)
+    rp_b[rng.choice(M, L, replace=False)] = 1
+    for i in np.flatnonzero(op_b):
+        dec.add_original_shard(int(i), b[i].tobytes())
+    for i in np.flatnonzero(rp_b):
+        dec.add_recovery_shard(int(i), rec_b[i].tobytes())
+    got = dict(dec.decode().restored_original_iter())
+    assert sorted(got) == [int(i) for i in np.flatnonzero(op_b == 0)]
+    bad = [i for i in got if got[i] != b[i].tobytes()]
+    assert not bad, f"object API decode: restored rows {bad[:8]} differ (stale staging read?)"
+    # the host pipeline with 0xEE in every absent input row
+    h_out = np.full((N, S), 0x33, np.uint8)
+    rs.decode_host(N, M, S, np.where(op_b[:, None] == 1, b, 0xEE).astype(np.uint8), op_b,
+                   np.where(rp_b[:, None] == 1, rec_b, 0xEE).astype(np.uint8), rp_b, h_out, slices=2,
+                   rate_=RATE[rate])
+    miss = op_b == 0
+    assert_rows_equal(h_out[miss], b[miss], "host pipeline decode")
+    assert np.all(h_out[~miss] == 0x33), "present rows of the output must not be written"
