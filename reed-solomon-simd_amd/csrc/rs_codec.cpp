@@ -9,10 +9,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <initializer_list>
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <string>
 #include <vector>
@@ -181,6 +185,96 @@ struct DeviceGuard {
     DeviceGuard &operator=(const DeviceGuard &) = delete;
 };
 
+// Host copies of the one-shot calls (rs_encode / rs_decode, lib.rs:251-353) on a few
+// helper threads: the caller's shards into the pinned staging and the recovery rows
+// out of it are ~1 MiB memcpy each at the headline shape, ~34 us on one core -- the
+// whole difference between the one-shot and the object API (BENCH r05 object_api).
+// run() hands out items [0, n) to the caller and the helpers and returns when every
+// item is done.  Helpers spin briefly for the next job (the one-shot's two copy
+// phases are ~40 us apart), then sleep.  RS_MI355X_COPY_THREADS = helper count
+// (default 7; 0: the caller copies alone).  Measured on MI355X boxes (1024:1024 x
+// 1 KiB one-shot encode, two rounds, profiles/r06e/oneshot_threads.txt): 0 helpers
+// 136 / 176 us, 1: 169 / 136, 3: 120 / 119, 7: 118 / 111 (object API 90-114 us).
+class CopyPool {
+  public:
+    explicit CopyPool(int helpers) {
+        for (int i = 0; i < helpers; ++i) th_.emplace_back([this] { worker(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_.store(true);
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    CopyPool(const CopyPool &) = delete;
+    CopyPool &operator=(const CopyPool &) = delete;
+    template <typename F>
+    void run(uint64_t n, const F &fn) {
+        if (n == 0) return;
+        if (th_.empty() || n == 1) {
+            for (uint64_t i = 0; i < n; ++i) fn(i);
+            return;
+        }
+        std::lock_guard<std::mutex> one(run_mu_);  // one job at a time per pool
+        Job job;
+        job.n = n;
+        job.call = [](const void *f, uint64_t i) { (*static_cast<const F *>(f))(i); };
+        job.fn = &fn;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_.store(&job);
+            gen_.fetch_add(1);
+        }
+        cv_.notify_all();
+        drain(job);
+        while (job.done.load() < n) __builtin_ia32_pause();
+        job_.store(nullptr);
+        while (users_.load() != 0) __builtin_ia32_pause();  // no helper still holds &job
+    }
+
+  private:
+    struct Job {
+        uint64_t n = 0;
+        void (*call)(const void *, uint64_t) = nullptr;
+        const void *fn = nullptr;
+        std::atomic<uint64_t> next{0}, done{0};
+    };
+    static void drain(Job &j) {
+        for (uint64_t i; (i = j.next.fetch_add(1)) < j.n;) {
+            j.call(j.fn, i);
+            j.done.fetch_add(1);
+        }
+    }
+    void worker() {
+        uint64_t seen = 0;
+        for (;;) {
+            const auto t0 = std::chrono::steady_clock::now();
+            while (gen_.load() == seen && !stop_.load()) {
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(100)) {
+                    std::unique_lock<std::mutex> lk(mu_);
+                    cv_.wait(lk, [&] { return gen_.load() != seen || stop_.load(); });
+                    break;
+                }
+                __builtin_ia32_pause();
+            }
+            if (stop_.load()) return;
+            seen = gen_.load();
+            users_.fetch_add(1);
+            if (Job *j = job_.load()) drain(*j);
+            users_.fetch_sub(1);
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_, run_mu_;
+    std::condition_variable cv_;
+    std::atomic<Job *> job_{nullptr};
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> users_{0};
+    std::atomic<bool> stop_{false};
+};
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -322,6 +416,17 @@ struct rs_context {
     std::mutex pool_mu;
     std::vector<rs_encoder_work *> enc_pool;
     std::vector<rs_decoder_work *> dec_pool;
+    // the one-shot calls' host copies (CopyPool), started on first use
+    std::once_flag copy_once;
+    std::unique_ptr<CopyPool> copy_pool;
+    CopyPool &copies() {
+        std::call_once(copy_once, [this] {
+            int helpers = 7;
+            if (const char *v = getenv("RS_MI355X_COPY_THREADS")) helpers = std::max(0, std::min(15, atoi(v)));
+            copy_pool.reset(new CopyPool(helpers));
+        });
+        return *copy_pool;
+    }
     bool prof = false;
     struct Rec {
         hipEvent_t a, b;
@@ -1102,7 +1207,20 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
         Mo.src[1] = orig_map;
         Mo.src_bstride[1] = g.orig_bstride;
         Mo.nsrc = 2;
-        Mo.dst = out_map;
+        // the destination map narrowed to the span of the erased originals: the
+        // waves holding no row of it after the FFT's last remap stop there
+        // (wave_stores), so at 1 % loss (11 restored rows of 2^11) one wave of 16
+        // runs the FFT's last in-wave layers, the reveal multiply and the stores
+        // instead of the 8 of the restored half (VALU accounting,
+        // profiles/r06c/valu_account.txt); present rows are never written either way
+        {
+            uint32_t lo = out_map.row_end, hi = out_map.row_begin;
+            for (uint32_t r = out_map.row_begin; r < out_map.row_end; ++r)
+                if (st[r] == 1) lo = std::min(lo, r), hi = r + 1;
+            Mo.dst = lo < hi ? rs::RowMap{out_map.base + uint64_t(lo - out_map.row_begin) * out_map.stride,
+                                          out_map.stride, lo, hi}
+                             : out_map;
+        }
         Mo.dst_bstride = g.out_bstride;
         Mo.fused_eval = 1;
         Mo.low_rate = high ? 0 : 1;
@@ -2111,8 +2229,11 @@ rs_status rs_decoder_reset(rs_decoder *d, uint64_t N, uint64_t M, uint64_t S, rs
     return decoder_configure(d, N, M, S, err);
 }
 
-static rs_status dec_add(rs_decoder *d, bool orig, uint64_t index, const uint8_t *shard, uint64_t len, rs_error *err) {
-    if (!d || (!shard && len)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+// copy = false (one-shot rs_decode): check and mark the shard only; the caller
+// copies the shards into the staging afterwards, in parallel
+static rs_status dec_add(rs_decoder *d, bool orig, uint64_t index, const uint8_t *shard, uint64_t len, rs_error *err,
+                         bool copy = true) {
+    if (!d || (copy && !shard && len)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     decoder_drop_result(d);
     const uint64_t count = orig ? d->N : d->M;
     std::vector<uint8_t> &present = orig ? d->orig_present : d->rec_present;
@@ -2134,7 +2255,7 @@ static rs_status dec_add(rs_decoder *d, bool orig, uint64_t index, const uint8_t
         if (err) err->shard_bytes = d->S, err->got = len;
         return RS_ERR_DIFFERENT_SHARD_SIZE;
     }
-    insert_row((orig ? d->h_orig : d->h_rec).p + index * d->row, shard, d->S);
+    if (copy) insert_row((orig ? d->h_orig : d->h_rec).p + index * d->row, shard, d->S);
     present[index] = 1;
     ++(orig ? d->orig_received : d->rec_received);
     return set_err(err, RS_OK);
@@ -2225,6 +2346,8 @@ void rs_decoder_work_free(rs_decoder_work *w) { delete w; }
 
 }  // extern "C"
 namespace {
+// rows per CopyPool item: >= 64 KiB of copies each
+uint64_t copy_rows_per_item(uint64_t S) { return std::max<uint64_t>(1, (uint64_t(64) << 10) / std::max<uint64_t>(1, S)); }
 template <typename W>
 W *pool_take(rs_context *ctx, std::vector<W *> &pool) {
     std::lock_guard<std::mutex> lock(ctx->pool_mu);
@@ -2265,10 +2388,25 @@ rs_status rs_encode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const u
     rs_encoder *e = nullptr;
     rs_status st = rs_encoder_new_with_work(ctx, RS_RATE_DEFAULT, N, M, S, pool_take(ctx, ctx->enc_pool), &e, err);
     if (st != RS_OK) return st;
-    for (uint64_t i = 0; i < given && st == RS_OK; ++i) st = rs_encoder_add_original_shard(e, original[i], S, err);
+    CopyPool &cp = ctx->copies();
+    const uint64_t per = copy_rows_per_item(S);
+    if (given <= N) {
+        // every shard is S bytes by this entry point's contract, so the per-shard checks
+        // (encoder_work.rs:56-65) cannot fail: the shards go into the staging in parallel
+        cp.run((given + per - 1) / per, [&](uint64_t k) {
+            for (uint64_t i = k * per; i < std::min(given, k * per + per); ++i)
+                insert_row(e->h_orig.p + i * e->row, original[i], S);
+        });
+        e->received = given;
+    } else {  // TooManyOriginalShards at shard N, after N were added (lib.rs:281-284)
+        for (uint64_t i = 0; i < given && st == RS_OK; ++i) st = rs_encoder_add_original_shard(e, original[i], S, err);
+    }
     if (st == RS_OK) st = rs_encoder_encode(e, err);
     if (st == RS_OK && recovery_out)
-        for (uint64_t i = 0; i < M; ++i) std::memcpy(recovery_out + i * S, rs_encoder_recovery(e, i), S);
+        cp.run((M + per - 1) / per, [&](uint64_t k) {
+            for (uint64_t i = k * per; i < std::min(M, k * per + per); ++i)
+                std::memcpy(recovery_out + i * S, rs_encoder_recovery(e, i), S);
+        });
     rs_encoder_work *w = nullptr;
     rs_encoder_into_parts(e, nullptr, &w);
     pool_put(ctx, ctx->enc_pool, w);
@@ -2296,18 +2434,38 @@ rs_status rs_decode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const u
     rs_status st = rs_decoder_new_with_work(ctx, RS_RATE_DEFAULT, N, M, S, pool_take(ctx, ctx->dec_pool), &d, err);
     if (st != RS_OK) return st;
     // shard lengths are S by construction of this C entry point; per-shard
-    // lengths are checked by the Python / C++ front-ends that know them
+    // lengths are checked by the Python / C++ front-ends that know them.  The
+    // indices are checked in the reference's order (decoder_work.rs:62-117) first,
+    // then the shards go into the staging in parallel (CopyPool)
     for (uint64_t i = 0; i < original_given && st == RS_OK; ++i)
-        st = rs_decoder_add_original_shard(d, original_index[i], original[i], S, err);
+        st = dec_add(d, true, original_index[i], nullptr, S, err, false);
     for (uint64_t i = 0; i < recovery_given && st == RS_OK; ++i)
-        st = rs_decoder_add_recovery_shard(d, recovery_index[i], recovery[i], S, err);
+        st = dec_add(d, false, recovery_index[i], nullptr, S, err, false);
+    CopyPool &cp = ctx->copies();
+    const uint64_t per = copy_rows_per_item(S), given = original_given + recovery_given;
+    if (st == RS_OK)
+        cp.run((given + per - 1) / per, [&](uint64_t k) {
+            for (uint64_t j = k * per; j < std::min(given, k * per + per); ++j) {
+                const bool o = j < original_given;
+                const uint64_t i = o ? j : j - original_given;
+                insert_row((o ? d->h_orig : d->h_rec).p + (o ? original_index : recovery_index)[i] * d->row,
+                           (o ? original : recovery)[i], S);
+            }
+        });
     if (st == RS_OK) st = rs_decoder_decode(d, err);
-    if (st == RS_OK && d->decoded)
+    if (st == RS_OK && d->decoded) {
+        std::vector<uint64_t> miss;
         for (uint64_t i = 0; i < N; ++i)
             if (!d->orig_present[i]) {
-                if (restored_out) std::memcpy(restored_out + i * S, rs_decoder_restored_original(d, i), S);
+                miss.push_back(i);
                 if (restored_mask) restored_mask[i] = 1;
             }
+        if (restored_out)
+            cp.run((miss.size() + per - 1) / per, [&](uint64_t k) {
+                for (uint64_t j = k * per; j < std::min<uint64_t>(miss.size(), k * per + per); ++j)
+                    std::memcpy(restored_out + miss[j] * S, rs_decoder_restored_original(d, miss[j]), S);
+            });
+    }
     rs_decoder_work *w = nullptr;
     rs_decoder_into_parts(d, nullptr, &w);
     pool_put(ctx, ctx->dec_pool, w);

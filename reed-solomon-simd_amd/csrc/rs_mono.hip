@@ -889,8 +889,10 @@ __device__ __forceinline__ void finish_col(uint32_t (&w)[2 << LR], uint32_t okm,
         if constexpr (E == 2) {
             c.lo[i] = __builtin_amdgcn_perm(w[2 * i + 1], w[2 * i], sel);
             if constexpr (SCALE) {
+#ifndef RS_MONO_SKIP_SCALEMUL  // tools/valu_account.sh ablation: no multiply of received rows
                 if constexpr (kQuadGather) c.lo[i] = quad_mul2(c.lo[i], st->t[i], lane);
                 else gf_mul2(c.lo[i], st->t[i]);
+#endif
                 if ((st->erased >> i) & 1u) c.lo[i] = 0;
             }
         } else {
@@ -963,7 +965,9 @@ __device__ __forceinline__ void store_col(const MonoCore &A, const uint32_t *row
             constexpr int i = decltype(ic)::value;
             if constexpr (E == 2) {
                 if (rt) {
+#ifndef RS_MONO_SKIP_REVEAL  // tools/valu_account.sh ablation: no reveal multiply
                     c.lo[i] = quad_mul2(c.lo[i], rt->t[i], lane);
+#endif
                     return;
                 }
             }
@@ -1130,6 +1134,9 @@ template <int L, int LR, int E>
 __device__ __forceinline__ void split_top(Col<L, LR, E> &c, uint32_t *plane, uint32_t *plane2, const uint32_t *tab_i,
                                           const uint32_t *tab_f, uint32_t lane, uint32_t wave, uint32_t out_half,
                                           bool zi = false, bool zf = false) {
+#ifdef RS_MONO_SKIP_SPLITTOP  // tools/valu_account.sh ablation (every wave skips it: no barrier is left waiting)
+    return;
+#endif
     zi = zi && RS_MONO_ZERO_TOP;
     zf = zf && RS_MONO_ZERO_TOP;
     using S = SeqOf<L, LR, true, true>;

@@ -1567,3 +1567,65 @@ def test_decode_ignores_absent_rows_and_stale_staging(torch, rs, rate, N, M, S):
     miss = op_b == 0
     assert_rows_equal(h_out[miss], b[miss], "host pipeline decode")
     assert np.all(h_out[~miss] == 0x33), "present rows of the output must not be written"
+
+
+# ---------------------------------------------------------------------------
+# the C ABI's one-shot rs_encode / rs_decode (lib.rs:251-353): shards copied into the
+# staging and results copied out on the context's helper threads (rs_codec.cpp CopyPool)
+
+def _c_oneshot(rs):
+    import ctypes
+    lib = rs._lib
+    u64, vp = ctypes.c_uint64, ctypes.c_void_p
+    lib.rs_encode.restype = ctypes.c_int
+    lib.rs_encode.argtypes = [vp, u64, u64, u64, vp, u64, vp, vp]
+    lib.rs_decode.restype = ctypes.c_int
+    lib.rs_decode.argtypes = [vp, u64, u64, u64, vp, vp, u64, vp, vp, u64, vp, vp, vp]
+    return lib
+
+
+def _ptrs(rows):
+    import ctypes
+    return (ctypes.c_void_p * max(1, len(rows)))(*[r.ctypes.data for r in rows])
+
+
+@pytest.mark.parametrize("N,M,S", [(1024, 1024, 1024), (3, 5, 64), (300, 200, 130), (100, 1000, 256), (5000, 300, 64)])
+def test_c_oneshot_matches_oracle(torch, rs, N, M, S):
+    import ctypes
+    lib = _c_oneshot(rs)
+    ctx = rs.default_context().handle
+    orig = O.generate_original(N, S, (N + M) & 0xFF)
+    want = O.encode("default", orig, M)
+    rows = [np.ascontiguousarray(orig[i]) for i in range(N)]
+    out = np.full((M, S), 0xEE, np.uint8)
+    err = rs._RsError()
+    for _ in range(2):  # the second call reuses the pooled working space
+        assert lib.rs_encode(ctx, N, M, S, _ptrs(rows), N, out.ctypes.data, ctypes.byref(err)) == 0
+        assert_rows_equal(out, want, "rs_encode")
+    rng = np.random.default_rng(N + 3 * M)
+    L = max(1, min(N, M) // 3)
+    lost = np.sort(rng.choice(N, L, replace=False))
+    have = np.setdiff1d(np.arange(N), lost)
+    ridx = np.sort(rng.choice(M, L, replace=False)).astype(np.uint64)
+    oidx = have.astype(np.uint64)
+    rrows = [np.ascontiguousarray(want[i]) for i in ridx]
+    orows = [rows[i] for i in have]
+    rest = np.full((N, S), 0x33, np.uint8)
+    mask = np.zeros(N, np.uint8)
+    assert lib.rs_decode(ctx, N, M, S, oidx.ctypes.data, _ptrs(orows), len(orows), ridx.ctypes.data, _ptrs(rrows),
+                         len(rrows), rest.ctypes.data, mask.ctypes.data, ctypes.byref(err)) == 0
+    assert np.array_equal(np.flatnonzero(mask), lost)
+    assert_rows_equal(rest[lost], orig[lost], "rs_decode")
+    assert np.all(rest[have] == 0x33)
+    # the reference's error order survives the checks-first / copies-after split
+    dup = np.concatenate([oidx[:2], oidx[:1]]).astype(np.uint64)
+    assert lib.rs_decode(ctx, N, M, S, dup.ctypes.data, _ptrs(orows[:3]), 3, ridx.ctypes.data, _ptrs(rrows),
+                         len(rrows), rest.ctypes.data, mask.ctypes.data, ctypes.byref(err)) == 2  # duplicate original
+    bad = np.array([N], np.uint64)
+    assert lib.rs_decode(ctx, N, M, S, bad.ctypes.data, _ptrs(orows[:1]), 1, ridx.ctypes.data, _ptrs(rrows),
+                         len(rrows), rest.ctypes.data, mask.ctypes.data, ctypes.byref(err)) == 4  # invalid index
+    assert err.index == N
+    extra = rows + rows[:1]
+    assert lib.rs_encode(ctx, N, M, S, _ptrs(extra), N + 1, out.ctypes.data, ctypes.byref(err)) == 9  # too many
+    assert lib.rs_encode(ctx, N, M, S, _ptrs(rows), N - 1 if N > 1 else 0, out.ctypes.data,
+                         ctypes.byref(err)) == 8  # too few

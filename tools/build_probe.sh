@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build a column-kernel probe binary tools/_probe/<name> from tools/mono_probe.hip
+# Build a column-kernel probe binary tools/probe_bin/<name> from tools/mono_probe.hip
 # (A/B tooling).  SRC: kernel source to include (default: the in-tree rs_mono.hip);
 # extra hipcc flags follow, e.g. -DRS_MONO_ONLY_L=11 -DRS_MONO_ONLY_MODE=2 for a
 # decode-only build in a fraction of the compile time.
@@ -8,8 +8,8 @@ set -euo pipefail
 NAME=$1; shift
 SRC=""
 if [[ "${1:-}" == SRC=* ]]; then SRC=$(realpath "${1#SRC=}"); shift; fi
-mkdir -p tools/_probe
+mkdir -p tools/probe_bin
 args=(--offload-arch=gfx950 -O3 -std=c++17 -Ireed-solomon-simd_amd/csrc "$@")
 if [ -n "$SRC" ]; then args+=("-DRS_MONO_SRC=\"$SRC\""); fi
-/opt/rocm/bin/hipcc "${args[@]}" tools/mono_probe.hip reed-solomon-simd_amd/csrc/gf_tables.cpp -o tools/_probe/$NAME
-echo built tools/_probe/$NAME
+/opt/rocm/bin/hipcc "${args[@]}" tools/mono_probe.hip reed-solomon-simd_amd/csrc/gf_tables.cpp -o tools/probe_bin/$NAME
+echo built tools/probe_bin/$NAME

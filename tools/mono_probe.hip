@@ -117,6 +117,10 @@ int main(int argc, char **argv) {
         const bool one = argv[3][1] == '1';
         // "...s": the split plan (restored rows = the upper half's erased originals)
         if (std::string(argv[3]).find('s') != std::string::npos) A.split = 1, A.out_half = 1;
+        // "...n": the destination narrowed to the erased rows' span, as rs_codec.cpp
+        // decode_dev passes it since r06 (1 %: the last 11 rows)
+        if (one && std::string(argv[3]).find('n') != std::string::npos)
+            A.dst = rs::RowMap{rec + size_t(n / 2 - 11) * S, S, n - 11, n};
         for (uint32_t r = 0; r < n; ++r) {
             const bool rcv = one ? (r < 12 || (r >= n / 2 && r < n - 11)) : r < n / 2;
             if (rcv) A.received[r >> 5] |= 1u << (r & 31);
