@@ -312,6 +312,10 @@ struct rs_context {
     // half launch stages a whole 2^11-row twiddle image per workgroup (~3 us of
     // load issue, profiles/r05e/half_stamps.txt) where a pass stages its sets' tables
     bool half = false, half_default = false;
+    // quad encode (try_quad below; rs_mono.hip kMonoQuadEnc): single-chunk 2-element
+    // encodes of 2^10 rows as the 4-element kernel of 2^9 pair rows (RS_MI355X_QUAD=0/1;
+    // rs_mono_enable + 2048: on, + 4096: off)
+    bool quad = false, quad_default = false;
     // multi-chunk encodes of 2^2..2^7-row transforms on k_chunks (use_chunks below;
     // RS_MI355X_CHUNKS=0/1; rs_mono_enable + 512: on, + 1024: off)
     bool chunks = true, chunks_default = true;
@@ -772,6 +776,25 @@ bool try_lane(rs_context *ctx, uint32_t L, uint32_t chunks, const rs::MonoArgs &
     return true;
 }
 
+// A single-chunk 2-element encode of 2^10 rows goes to the quad form of the column
+// kernel (rs_mono.hip kMonoQuadEnc: the 4-element kernel of 2^9 pair rows, each
+// pack 2 elements x 2 rows) when enabled; false: not taken.  Its images: the
+// 4-element tables of layers >= 1 (the 2^L-row image from slot 2^(L-1) on) and
+// the 2-element layer-0 tables (A.lut).
+bool try_quad(rs_context *ctx, uint32_t L, uint32_t chunks, const rs::MonoArgs &M, hipStream_t s, uint64_t bytes) {
+    if (!ctx->quad || chunks != 1 || M.elems != 2 || !rs::quad_supported(int(L))) return false;
+    rs::MonoArgs Q = M;
+    const uint64_t n = uint64_t(1) << L;
+    Q.img = mono_images(ctx, L, 4) + (n / 2) * rs::kPermWords;
+    Q.img_words = (n - 1) * rs::kPermWords;
+    Q.lut = mono_images(ctx, L, 2);
+    hipEvent_t ev = nullptr;
+    if (t_prof_ctx) prof_begin(s, &ev);
+    check(rs::launch_quad(int(L), Q, s));
+    if (t_prof_ctx) prof_end(s, ev, rs::launch_name_buf(), bytes);
+    return true;
+}
+
 // Multi-chunk encodes of small transforms (rs_chunks.hip): one launch in which the
 // waves of a pack's workgroup take the chunks in parallel (HighRate input chunks,
 // LowRate output chunks), twiddle tables built in LDS from basis images.  One
@@ -922,7 +945,8 @@ void encode_high(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint
         Mo.ifft_img_step = 1;
         Mo.fft_img = 0;
         const uint64_t bytes = (N + M) * uint64_t(g.packs) * 8 * g.stripes;
-        if (!try_lane(ctx, L, C, Mo, s, bytes)) launch_mono(rs::kMonoEncodeHigh, L, Mo, s, bytes);
+        if (!try_quad(ctx, L, C, Mo, s, bytes) && !try_lane(ctx, L, C, Mo, s, bytes))
+            launch_mono(rs::kMonoEncodeHigh, L, Mo, s, bytes);
         return;
     }
     if (use_chunks(ctx, L, g, C, true)) {
@@ -1014,7 +1038,8 @@ void encode_low(rs_context *ctx, Workspace &ws, const Geom &g, uint64_t N, uint6
         Mo.fft_img = 1;  // output chunk c: skew offset c * n + n
         Mo.fft_img_step = 1;
         const uint64_t bytes = (N + M) * uint64_t(g.packs) * 8 * g.stripes;
-        if (!try_lane(ctx, L, C, Mo, s, bytes)) launch_mono(rs::kMonoEncodeLow, L, Mo, s, bytes);
+        if (!try_quad(ctx, L, C, Mo, s, bytes) && !try_lane(ctx, L, C, Mo, s, bytes))
+            launch_mono(rs::kMonoEncodeLow, L, Mo, s, bytes);
         return;
     }
     if (use_chunks(ctx, L, g, C, false)) {
@@ -1674,6 +1699,8 @@ rs_status rs_context_create(int device, rs_context **out) {
         ctx->lane_default = ctx->lane;
         if (const char *hs = getenv("RS_MI355X_HALF")) ctx->half = hs[0] == '1';
         ctx->half_default = ctx->half;
+        if (const char *qs = getenv("RS_MI355X_QUAD")) ctx->quad = qs[0] == '1';
+        ctx->quad_default = ctx->quad;
         if (const char *ck = getenv("RS_MI355X_CHUNKS")) {  // 0 off, 1 default routing, 2 every supported shape
             ctx->chunks = ck[0] != '0';
             ctx->chunks_forced = ck[0] == '2';
@@ -2635,6 +2662,8 @@ rs_status rs_mono_enable(rs_context *ctx, int enable) {
     ctx->lane_max_l = (enable & 32) ? 10 : ctx->lane_max_l_default;
     // + 128: half-split 2^12-row transforms on, + 256: off
     ctx->half = (enable & 128) ? true : (enable & 256) ? false : ctx->half_default;
+    // + 2048: quad encode on, + 4096: off
+    ctx->quad = (enable & 2048) ? true : (enable & 4096) ? false : ctx->quad_default;
     // + 512: multi-chunk kernel on, + 1024: off
     ctx->chunks = (enable & 512) ? true : (enable & 1024) ? false : ctx->chunks_default;
     // (neither bit: the context's defaults, RS_MI355X_CHUNKS=2's forced routing included)

@@ -229,6 +229,12 @@ enum MonoMode {
     kMonoHalfIDec = 4,
     kMonoHalfFEnc = 5,
     kMonoHalfFDec = 6,
+    // quad encode (launch_quad): a single-chunk encode of 2^L rows in 2-element
+    // column packs run as the 4-element kernel of 2^(L-1) "pair rows": a pack is
+    // 2 elements x rows (2q, 2q + 1), so every layer above row bit 0 multiplies 4
+    // elements per table (gf_muladd4, 26 VALU) where the 2-element kernel spends
+    // 2 x 24 on them; layer 0 (inside the pack) runs first / last on its own.
+    kMonoQuadEnc = 7,
 };
 constexpr uint32_t kMonoFusedRows = 2048;  // largest work size of the fused-eval_poly decode
 // The kernel arguments of every column kernel; the staged decode's kernels take
@@ -281,6 +287,12 @@ bool chunks_supported(int L);
 hipError_t launch_chunks(int L, bool high, const MonoCore &A, hipStream_t stream, int pw = 1);
 // kMonoHalf* modes: L = 11 only, one stripe, grid.y = halves (launch_mono_half).
 hipError_t launch_mono_half(int mode, uint32_t halves, const MonoArgs &A, hipStream_t stream);
+// Quad encode of 2^L rows (kMonoQuadEnc; quad_supported(L)): packs / fmt / rows of
+// the 2-element format; img = the 4-element images of 2^L rows offset by 2^(L-1)
+// tables (layer 0 skipped), img_words = (2^L - 1) * 20; lut = the 2-element images
+// of 2^L rows (their layer-0 tables); one chunk; stripes for a batch.
+bool quad_supported(int L);
+hipError_t launch_quad(int L, const MonoArgs &A, hipStream_t stream);
 // Variant launch_mono picks: LDS-staged twiddles (single chunk, 2 rows per
 // lane, L <= 11); fused_eval and stripes > 1 require it.
 bool mono_staged(int L, uint32_t chunks);

@@ -1021,6 +1021,121 @@ __device__ __forceinline__ void store_col(const MonoCore &A, const uint32_t *row
     });
 }
 
+// ---------------------------------------------------------------------------
+// Quad encode (kMonoQuadEnc, rs_device.hpp): the 4-element kernel of 2^L "pair
+// rows" runs the 2^(L+1)-row encode of a 2-element column pack.  Pair row q's
+// pack = [lo(2q, e0) lo(2q, e1) lo(2q+1, e0) lo(2q+1, e1)] + the high bytes
+// likewise: rows 2q and 2q + 1 share every twiddle above row bit 0 (the group of
+// layer x >= 1 is row >> (x + 1) = q >> x), so layer x of the rows is layer x - 1
+// of the pair rows, with the 2^(L+1)-row image's tables of layers >= 1 (the host
+// offsets A.img by the layer-0 tables).  Layer 0 -- the butterflies inside a
+// pack -- runs before the IFFT and after the FFT (quad_layer0), on 2-element
+// tables staged per wave (kQuad0Slot).
+constexpr uint32_t kQuad0Slot = 20;  // words per staged layer-0 table (16 used; 80-B slots spread the banks)
+
+// Row loads of the lane's paired words: word j of pair row Q = its plane's
+// 16-bit halves of rows 2Q (bits 0-15) and 2Q + 1 (bits 16-31), each read as the
+// aligned dword around it (finish_quad picks the half), 2 loads per word.
+template <int L, int LR, int PK>
+__device__ __forceinline__ void issue_quad(const MonoCore &A, const PackIO &io, const StripeBases &sb,
+                                           uint32_t (&w)[4 << LR], uint32_t &okm, uint32_t lane, uint32_t wave) {
+    using S = SeqOf<L, LR, false, PK>;
+    const uint32_t off = io.lo + ((lane & 1u) ? io.hi_delta : 0u);
+    const uint8_t *any_row = A.src[0].row_end > A.src[0].row_begin ? sb.src0 : sb.src1;
+    okm = 0;
+    const RowBase rb = row_base(A, sb, 2u * paired_row<S, 0, LR>(lane, wave, 0));
+    static_for<0, (2 << LR)>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        static_for<0, 2>([&](auto hc) {
+            constexpr int h = decltype(hc)::value;
+            const uint8_t *p = row_at<2u * paired_delta<S, 0, LR>(j) + uint32_t(h)>(A, rb);
+            const bool ok = p != nullptr;
+            const uint8_t *a = (ok ? p : any_row) + off;
+            uint32_t v;
+            if (io.bytes) v = ld_half(a, io);
+            else v = *reinterpret_cast<const uint32_t *>(a - (reinterpret_cast<uintptr_t>(a) & 3u));
+#if defined(RS_MONO_SKIP_IO) || defined(RS_MONO_SKIP_LOADS)
+            v = (rb.r0 + 2u * paired_delta<S, 0, LR>(j) + uint32_t(h)) * 0x9E3779B9u + off;
+#endif
+            okm |= uint32_t(ok) << (2 * j + h);
+            w[2 * j + h] = v;
+        });
+    });
+}
+// halves -> pair-row words (rows outside the caller's matrices are zero), then
+// the 4-element finish (paired words -> each lane's own pair rows)
+template <int L, int LR>
+__device__ __forceinline__ void finish_quad(uint32_t (&w)[4 << LR], uint32_t okm, Col<L, LR, 4> &c, uint32_t lane,
+                                            const PackIO &io) {
+    const uint32_t sel = !io.bytes && (io.lo & 2u) ? 0x07060302u : 0x05040100u;
+    uint32_t x[2 << LR];
+    static_for<0, (2 << LR)>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const uint32_t h0 = (okm >> (2 * j)) & 1u ? w[2 * j] : 0u, h1 = (okm >> (2 * j + 1)) & 1u ? w[2 * j + 1] : 0u;
+        x[j] = io.bytes ? (h0 & 0xFFFFu) | (h1 << 16) : __builtin_amdgcn_perm(h1, h0, sel);
+    });
+    finish_col<L, LR, false, 4>(x, ~0u, nullptr, c, lane, io);
+}
+// Stores of the pair rows that fall in A.dst (placement: end of the FFT): each
+// word's halves to rows 2Q and 2Q + 1, paired like the loads
+template <int L, int LR, int PK>
+__device__ __forceinline__ void store_quad(const MonoCore &A, const PackIO &io, const StripeBases &sb,
+                                           const Col<L, LR, 4> &c, uint32_t lane, uint32_t wave) {
+    using S = SeqOf<L, LR, true, PK>;
+    constexpr int I = S::v.count;
+    constexpr int R = 1 << LR;
+    uint32_t w[2 * R];
+    static_for<0, R>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        w[2 * i] = c.lo[i];
+        w[2 * i + 1] = c.hi[i];
+        xpose<0>(w[2 * i], w[2 * i + 1], lane);
+    });
+    const uint32_t off = io.lo + ((lane & 1u) ? io.hi_delta : 0u);
+    const uint32_t r0 = 2u * paired_row<S, I, LR>(lane, wave, 0);
+    uint8_t *const p0 = const_cast<uint8_t *>(map_base(A.dst, sb.dst, r0));  // (see row_at)
+    static_for<0, 2 * R>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        static_for<0, 2>([&](auto hc) {
+            constexpr int h = decltype(hc)::value;
+            constexpr uint32_t D = 2u * paired_delta<S, I, LR>(j) + uint32_t(h);
+            const uint32_t r = r0 + D;
+#if defined(RS_MONO_SKIP_IO) || defined(RS_MONO_SKIP_STORES)
+            if (w[j] == 0x12345678u)
+#endif
+            if (r - A.dst.row_begin < A.dst.row_end - A.dst.row_begin)
+                st_half(p0 + uint64_t(D) * A.dst.stride + off, h ? w[j] >> 16 : w[j] & 0xFFFFu, io);
+        });
+    });
+}
+// Layer 0 of the rows (engine_naive.rs:96-100 IFFT / :64-68 FFT) on the lane's
+// pair rows: a = row 2Q (bytes 0-1 of both planes), b = row 2Q + 1 (bytes 2-3),
+// table t of group Q (the 2^(L+1)-row image's layer-0 slot Q, staged at `tabs`)
+template <int L, int LR, typename S, int I, bool FFT>
+__device__ __forceinline__ void quad_layer0(Col<L, LR, 4> &c, const uint32_t *tabs, uint32_t lane, uint32_t wave) {
+    constexpr int R = 1 << LR;
+    constexpr uint32_t W = 1u << (LR + 6);
+    const uint32_t a0 = lane_rows<S, I>(lane, wave);
+    static_for<0, R>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const uint32_t q = (a0 | reg_rows<S, I, LR>(i)) & (W - 1u);
+        uint32_t t[16];
+        const uint4 *p = reinterpret_cast<const uint4 *>(tabs + q * kQuad0Slot);
+        static_for<0, 4>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const uint4 v = p[k];
+            t[4 * k] = v.x, t[4 * k + 1] = v.y, t[4 * k + 2] = v.z, t[4 * k + 3] = v.w;
+        });
+        // 2-element words [lo0 lo1 hi0 hi1] of the two rows
+        uint32_t a = __builtin_amdgcn_perm(c.hi[i], c.lo[i], 0x05040100u);
+        uint32_t b = __builtin_amdgcn_perm(c.hi[i], c.lo[i], 0x07060302u);
+        if constexpr (FFT) fft_bfly2(a, b, t);
+        else ifft_bfly2(a, b, t);
+        c.lo[i] = __builtin_amdgcn_perm(b, a, 0x05040100u);
+        c.hi[i] = __builtin_amdgcn_perm(b, a, 0x07060302u);
+    });
+}
+
 // Formal derivative, closed form over the whole column (src/engine/utils.rs:99-104):
 //   out[q] = x[q] ^ XOR_{b < L, q_b = 0} x[q | 2^b]   (placement: end of the IFFT)
 // Terms on register bits come from the lane's own registers, terms on lane
@@ -1518,7 +1633,7 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
         A.src_bstride[1] = K.src_bstride[1];
         A.dst_bstride = K.dst_bstride;
     }
-    if constexpr (MODE >= kMonoHalfIEnc) {  // half-split kernels
+    if constexpr (MODE >= kMonoHalfIEnc && MODE <= kMonoHalfFDec) {  // half-split kernels
         A.half0 = K.half0;
         A.zero_halves = K.zero_halves;
         A.top_i = K.top_i;
@@ -1549,7 +1664,8 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
     const StripeBases sb = BATCH ? stripe_bases(A, blockIdx.y) : StripeBases{A.src[0].base, A.src[1].base,
                                                                              const_cast<uint8_t *>(A.dst.base)};
     // the pack's bytes in the caller's rows (tails: shards.rs:38-74)
-    const PackIO io = E == 4 ? pack_io(A.fmt, pk) : pack_io2(A.fmt, pk);
+    // (quad encode: 2-element column packs, computed as 4-element pair-row packs)
+    const PackIO io = E == 4 && MODE != kMonoQuadEnc ? pack_io(A.fmt, pk) : pack_io2(A.fmt, pk);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // half-split modes (kMonoHalf*): this workgroup's half; its transform uses one
@@ -1581,6 +1697,7 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             // 0 of phases 1 / 3 from the image when Stage::B0)
             constexpr bool DEC = MODE == kMonoDecode;
             constexpr bool HSC = MODE == kMonoHalfIDec, HFD = MODE == kMonoHalfFDec;
+            constexpr bool QUAD = MODE == kMonoQuadEnc;  // (quad encode: see issue_quad)
             // the half-split kernels' work rows: whole 64-byte blocks
             const PackIO io_w = E == 4 ? pack_io(ShardFormat{}, pk) : pack_io2(ShardFormat{}, pk);
             uint32_t *shared = lds + G::plane_words;
@@ -1660,6 +1777,41 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             // kMonoHalfF: the two halves' IFFT rows (work rows, placement at the FFT's start)
             uint32_t w2[2 << LR] = {};
             uint32_t okm2 = 0;
+            // quad encode: the rows' 16-bit halves (issue_quad), and layer 0's tables of the
+            // wave's 2^IW pair rows for the IFFT (image ii) and the FFT (fi): 2-element
+            // tables of the 2^(L+1)-row images (A.lut), staged in the wave's two regions
+            uint32_t wq[4 << LR] = {};
+            uint32_t okmq = 0;
+            constexpr uint32_t QW = 1u << G::IW;                   // pair rows (layer-0 tables) per wave
+            constexpr int KQ = QUAD ? int((4 * QW + 63) / 64) : 1;  // 16-byte pieces per lane per transform
+            uint4 vq[2][KQ];
+            uint32_t *const qtab = lds + G::words_enc + wave * 2u * QW * kQuad0Slot;
+            auto issue_quad_tabs = [&]() {
+                if constexpr (QUAD) {
+                    constexpr uint64_t kImg2 = uint64_t((2u << L) - 1u) * 16u;  // words per 2-element image
+                    static_for<0, 2>([&](auto fc) {
+                        constexpr int f = decltype(fc)::value;
+                        const uint4 *src = reinterpret_cast<const uint4 *>(A.lut + (f ? fi : ii) * kImg2) +
+                                           uint64_t(wave) * QW * 4u;
+                        static_for<0, KQ>([&](auto kc) {
+                            const uint32_t q = lane + 64u * decltype(kc)::value;
+                            vq[f][kc] = ld_piece(src + (q < 4 * QW ? q : 4 * QW - 1));
+                        });
+                    });
+                }
+            };
+            auto write_quad_tabs = [&]() {
+                if constexpr (QUAD)
+                    static_for<0, 2>([&](auto fc) {
+                        constexpr int f = decltype(fc)::value;
+                        static_for<0, KQ>([&](auto kc) {
+                            const uint32_t q = lane + 64u * decltype(kc)::value;
+                            if (q < 4 * QW)
+                                reinterpret_cast<uint4 *>(qtab + f * QW * kQuad0Slot + (q >> 2) * kQuad0Slot)[q & 3u] =
+                                    vq[f][kc];
+                        });
+                    });
+            };
             // phase-1 tables (a live wave loads all of its region's pieces; lanes past
             // the region's end re-read its last piece and do not write it, so the
             // loads are unconditional); B0: layer 0's go into the region first, the
@@ -1728,9 +1880,11 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 issue_priv();
                 issue_shared();
             } else if constexpr (!DEC) {
-                issue_rows(kIO{});
+                if constexpr (QUAD) issue_quad<L, LR, PK>(A, io, sb, wq, okmq, lane, wave);
+                else issue_rows(kIO{});
                 issue_priv();
                 issue_shared();
+                issue_quad_tabs();
             } else {
                 if constexpr (kShFirst) issue_shared();
                 RS_MSTAMP(16);
@@ -1793,11 +1947,15 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 const uint32_t q = threadIdx.x + T * decltype(kc)::value;
                 if (q < LPC * kSh) G::put(shared, q, vs[kc], [](uint32_t p) { return G::atS(p); });
             });
+            write_quad_tabs();  // (wave-private: read back by this wave only)
 #endif
             C cb;  // kMonoHalfF: the upper half's rows
             if constexpr (HALF_F) {
                 finish_col<L, LR, false>(w, okm, &st, c, lane, io_w);
                 finish_col<L, LR, false>(w2, okm2, &st, cb, lane, io_w);
+            } else if constexpr (QUAD) {
+                finish_quad<L, LR>(wq, okmq, c, lane, io);
+                quad_layer0<L, LR, SeqOf<L, LR, false, PK>, 0, false>(c, qtab, lane, wave);  // IFFT layer 0 of the rows
             } else {
                 finish_col<L, LR, DEC || HSC>(w, okm, &st, c, lane, io);
             }
@@ -1980,8 +2138,14 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                                                              fi == 0);
             }
             RS_MSTAMP(10);
-            store_col<L, LR, DEC || HFD, PK>(A, ri, HALF_F ? hh : 0u, io, sb, c, lane, wave,
-                                             kPreReveal && G::WB > 0 ? &rt : nullptr);
+            if constexpr (QUAD) {
+                using SQ = SeqOf<L, LR, true, PK>;
+                quad_layer0<L, LR, SQ, SQ::v.count, true>(c, qtab + QW * kQuad0Slot, lane, wave);  // FFT layer 0
+                store_quad<L, LR, PK>(A, io, sb, c, lane, wave);
+            } else {
+                store_col<L, LR, DEC || HFD, PK>(A, ri, HALF_F ? hh : 0u, io, sb, c, lane, wave,
+                                                 kPreReveal && G::WB > 0 ? &rt : nullptr);
+            }
             RS_MSTAMP(11);
       };
       if constexpr (MODE == kMonoDecode) {
@@ -2161,6 +2325,39 @@ hipError_t launch_mono_half(int mode, uint32_t halves, const MonoArgs &A, hipStr
                                                     : go(std::integral_constant<int, kMonoHalfFDec>{}, I4{});
             default: return hipErrorNotSupported;
         }
+    }
+}
+
+// Quad encode (kMonoQuadEnc): 2^10 rows as the 4-element kernel of 2^9 pair rows,
+// 256 threads.  (2^11 rows would need 8 waves' layer-0 regions: 160 KiB of LDS
+// with the kernel's own 90 KiB.)
+bool quad_supported(int L) { return L == 10 && RS_MONO_HAS_L(9) && RS_MONO_HAS_MODE(kMonoQuadEnc); }
+
+hipError_t launch_quad(int L, const MonoArgs &A, hipStream_t s) {
+    if (A.packs == 0) return hipSuccess;
+    if (!quad_supported(L) || A.chunks != 1) return hipErrorInvalidValue;
+    if constexpr (!(RS_MONO_HAS_L(9) && RS_MONO_HAS_MODE(kMonoQuadEnc))) {
+        return hipErrorNotSupported;
+    } else {
+        auto go = [&](auto bc) -> hipError_t {
+            constexpr bool BATCH = decltype(bc)::value;
+            constexpr int LQ = 9, LR = mono_lr(LQ, true), MODE = kMonoQuadEnc;
+            using G = Stage<LQ, LR, mono_pk(MODE, true, false), 4>;
+            constexpr uint32_t QW = 1u << G::IW;
+            const size_t lds = (size_t(G::words_enc) + size_t(G::kWaves) * 2u * QW * kQuad0Slot) * 4u;
+            static_assert((size_t(G::words_enc) + size_t(G::kWaves) * 2u * QW * kQuad0Slot) * 4u <= 160u * 1024u,
+                          "quad encode: LDS per workgroup");
+            static std::atomic<uint64_t> attr_devs{0};
+            hipError_t e = lds_attr_once(attr_devs, reinterpret_cast<const void *>(&k_mono<LQ, LR, MODE, true, BATCH, false, 4>),
+                                         int(lds));
+            if (e != hipSuccess) return e;
+            k_mono<LQ, LR, MODE, true, BATCH, false, 4>
+                <<<dim3(8u * A.packs_per_xcd, BATCH ? A.stripes : 1), 1 << (LQ - LR), lds, s>>>(static_cast<const MonoCore &>(A));
+            snprintf(launch_name_buf(), kLaunchNameBytes, "k_mono<%d, %d, %d, true, %s, false, 4>", LQ, LR, MODE,
+                     BATCH ? "true" : "false");
+            return hipGetLastError();
+        };
+        return A.stripes > 1 ? go(std::true_type{}) : go(std::false_type{});
     }
 }
 

@@ -976,6 +976,58 @@ def test_lane_kernel_encode_matches_oracle(torch, rs, rate, N, M, S):
 
 
 # ---------------------------------------------------------------------------
+# quad encode (rs_mono.hip kMonoQuadEnc, rs_codec.cpp try_quad): single-chunk 2-element
+# encodes of 2^10 rows as the 4-element kernel of 2^9 pair rows (pack = 2 elements x rows
+# 2q, 2q + 1), layer 0 inside the packs before the IFFT and after the FFT
+
+QUAD_CASES = [
+    # (rate, N, M, S): 2^10-row transforms, one chunk; tails, odd row counts, both rates
+    ("high", 1024, 1024, 1024), ("high", 1000, 1000, 576), ("high", 1, 513, 64), ("high", 600, 1000, 130),
+    ("high", 1023, 1021, 6), ("high", 1024, 600, 2), ("low", 1024, 1024, 256), ("low", 1000, 600, 192),
+    ("low", 513, 7, 66), ("default", 700, 999, 1000),
+]
+
+
+@pytest.mark.parametrize("rate,N,M,S", QUAD_CASES)
+def test_quad_encode_matches_oracle(torch, rs, rate, N, M, S):
+    rs.mono_enable(1 | 2048)
+    try:
+        orig = O.generate_original(N, S, (N + 3 * M + S) & 0xFF)
+        want = O.encode(rate, orig, M)
+        d_o = _dev(torch, orig)
+        d_r = torch.full((M, S), 0xEE, dtype=torch.uint8, device="cuda")
+        route = _route_of(torch, rs, lambda: rs.encode_device(N, M, S, d_o, d_r, rate_=RATE[rate]))
+        assert len(route) == 1 and route[0].startswith("k_mono<9, 1, 7,"), route
+        assert_rows_equal(d_r.cpu().numpy(), want, "quad encode")
+        # strided rows: column slices of wider matrices (the rows' base and stride differ)
+        wo = torch.full((N, S + 64), 0x11, dtype=torch.uint8, device="cuda")
+        wr = torch.full((M, S + 64), 0x22, dtype=torch.uint8, device="cuda")
+        wo[:, 32:32 + S] = d_o
+        rs.encode_device(N, M, S, wo[:, 32:32 + S], wr[:, 32:32 + S], rate_=RATE[rate])
+        torch.cuda.synchronize()
+        got = wr.cpu().numpy()
+        assert_rows_equal(got[:, 32:32 + S], want, "quad encode, strided")
+        assert np.all(got[:, :32] == 0x22) and np.all(got[:, 32 + S:] == 0x22)
+        # a batch of 3 stripes in one launch (2-element packs while packs x stripes fit)
+        if S <= 1024:
+            origs = [orig] + [O.generate_original(N, S, 70 + b) for b in range(2)]
+            b_o = _dev(torch, np.stack(origs))
+            b_r = torch.empty((3, M, S), dtype=torch.uint8, device="cuda")
+            rs.encode_device_batch(N, M, S, b_o, b_r, rate_=RATE[rate])
+            torch.cuda.synchronize()
+            for b in range(3):
+                assert_rows_equal(b_r[b].cpu().numpy(), O.encode(rate, origs[b], M), f"quad batch stripe {b}")
+        # quad off: the 2-element column kernel, the same bytes
+        rs.mono_enable(1 | 4096)
+        d_r2 = torch.full((M, S), 0x77, dtype=torch.uint8, device="cuda")
+        route = _route_of(torch, rs, lambda: rs.encode_device(N, M, S, d_o, d_r2, rate_=RATE[rate]))
+        assert not any(r.startswith("k_mono<9, 1, 7,") for r in route), route
+        assert torch.equal(d_r, d_r2)
+    finally:
+        rs.mono_enable(1)
+
+
+# ---------------------------------------------------------------------------
 # multi-chunk encodes of 2^2..2^7-row transforms in one launch (rs_chunks.hip k_chunks): the
 # waves of a pack's workgroup take HighRate input chunks / LowRate output chunks in parallel
 # (routed by default where it measured faster, rs_codec.cpp use_chunks; rs_mono_enable + 512
