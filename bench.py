@@ -188,6 +188,14 @@ def main():
         sharded_bench(args, rs, ctx, world, rank, dev)
     else:
         stripe_bench(args, rs, ctx, config, world, rank, dev)
+    if os.environ.get("RS_BENCH_REHEARSE") == "1":
+        # the rehearsal's memory record (stderr): this rank's peak of torch allocations, and
+        # the device's memory in use (all ranks share the one GPU, the library's own
+        # buffers included) as each rank finishes
+        free, total = torch.cuda.mem_get_info(dev)
+        print(json.dumps({"rank": rank, "world": world,
+                          "torch_max_allocated_GiB": round(torch.cuda.max_memory_allocated(dev) / 2**30, 3),
+                          "device_used_GiB_all_ranks": round((total - free) / 2**30, 3)}), file=sys.stderr, flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -21,3 +21,6 @@ for q in ("0", "1"):
     for k in sorted(acc):
         print("quad" if q == "1" else "e2", k[0], k[1], round(acc[k][0] / len(acc[k][1])))
 PY
+# world 8 rehearsal of bench.py --gpus 8 on this one GPU (gloo collectives; numbers meaningless)
+RS_BENCH_REHEARSE=1 timeout -k 10 600 python -u bench.py --gpus 8 --steps 3 --warmup 1 --no-cpu --no-host --no-object --no-copy --batch 1 > $O/rehearse8.log 2>&1
+rc=$?; grep -E '^\{"metric|"rank"' $O/rehearse8.log | cut -c1-400; exit $rc
