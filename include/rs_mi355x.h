@@ -337,7 +337,11 @@ rs_status rs_check_device(rs_context *ctx);
  * take the chunks in parallel (rs_chunks.hip; RS_MI355X_CHUNKS=0 at context
  * creation: never) where that measured faster: all of them but LowRate
  * encodes of more than 8 output chunks in 2-element packs.  Adding 512 sends
- * every multi-chunk encode of those sizes there, adding 1024 none.
+ * every multi-chunk encode of those sizes there, adding 1024 none.  Adding
+ * 2048 runs single-chunk 2-element encodes of 2^10 rows as the 4-element
+ * kernel of 2^9 pair rows (the quad encode; off by default: bit-exact but
+ * slower; RS_MI355X_QUAD=1 at context creation: on), adding 4096 turns it off.
+ * Neither bit of a pair: the context's defaults (its environment included).
  * A/B and tests; results are identical in every mode. */
 rs_status rs_mono_enable(rs_context *ctx, int enable);
 

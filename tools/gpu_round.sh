@@ -5,6 +5,7 @@
 # Usage (from the repo root, on the box):  bash tools/gpu_round.sh <tag> [pytest-args...]
 #   SKIP_TESTS=1   skip the GPU test suite
 #   CONFIGS=1      also the other single-GPU BASELINE configs (3, 4, 5 at N = 1)
+#   SHAPES=1       also the reference README's shape table (bench.py --shape-table)
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -euo pipefail
 TAG=${1:-r02}
@@ -40,7 +41,7 @@ profile() {  # profile <config-name> <bench args...>
   echo "profiled $cfg"
 }
 
-profile 1024x1024x1k --no-cpu --no-host --no-copy --no-sharded --batch 1 --steps 200 --warmup 20
+profile 1024x1024x1k --no-cpu --no-host --no-copy --no-sharded --no-configs --batch 1 --steps 200 --warmup 20
 if [ "${CONFIGS:-0}" = "1" ]; then  # the other single-GPU BASELINE configs
   timeout -k 10 300 python -u bench.py --no-cpu --config 32768x32768x1k --steps 50 --warmup 5 \
     > "$OUT/bench_config3.json" 2>> "$OUT/bench.err"
@@ -51,5 +52,8 @@ if [ "${CONFIGS:-0}" = "1" ]; then  # the other single-GPU BASELINE configs
   profile 32768x32768x1k --no-cpu --no-host --no-copy --batch 1 --config 32768x32768x1k --steps 20 --warmup 3
   profile 8192x8192x64k --no-cpu --no-host --no-copy --batch 1 --config 8192x8192x64k --steps 5 --warmup 2
   profile 32768x32768x64k --no-cpu --config 32768x32768x64k --steps 5 --warmup 2 --profile-steps 30
+fi
+if [ "${SHAPES:-0}" = "1" ]; then  # the reference README's shape table
+  timeout -k 10 300 python -u bench.py --shape-table --steps 50 > "$OUT/shape_table.json" 2>> "$OUT/bench.err"
 fi
 echo "gpu_round $TAG done"
