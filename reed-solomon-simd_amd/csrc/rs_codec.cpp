@@ -420,6 +420,9 @@ struct rs_context {
     std::mutex pool_mu;
     std::vector<rs_encoder_work *> enc_pool;
     std::vector<rs_decoder_work *> dec_pool;
+    // one-shot shard copies in on the CopyPool too (RS_MI355X_COPYIN_POOL=0: on the calling
+    // thread only; the results always go out on the pool)
+    bool copyin_pool = true;
     // the one-shot calls' host copies (CopyPool), started on first use
     std::once_flag copy_once;
     std::unique_ptr<CopyPool> copy_pool;
@@ -1700,6 +1703,7 @@ rs_status rs_context_create(int device, rs_context **out) {
         if (const char *hs = getenv("RS_MI355X_HALF")) ctx->half = hs[0] == '1';
         ctx->half_default = ctx->half;
         if (const char *qs = getenv("RS_MI355X_QUAD")) ctx->quad = qs[0] == '1';
+        if (const char *cp = getenv("RS_MI355X_COPYIN_POOL")) ctx->copyin_pool = cp[0] == '1';
         ctx->quad_default = ctx->quad;
         if (const char *ck = getenv("RS_MI355X_CHUNKS")) {  // 0 off, 1 default routing, 2 every supported shape
             ctx->chunks = ck[0] != '0';
@@ -2420,14 +2424,22 @@ rs_status rs_encode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const u
     if (given <= N) {
         // every shard is S bytes by this entry point's contract, so the per-shard checks
         // (encoder_work.rs:56-65) cannot fail: the shards go into the staging in parallel
-        cp.run((given + per - 1) / per, [&](uint64_t k) {
+        auto in = [&](uint64_t k) {
             for (uint64_t i = k * per; i < std::min(given, k * per + per); ++i)
                 insert_row(e->h_orig.p + i * e->row, original[i], S);
-        });
+        };
+        const uint64_t items = (given + per - 1) / per;
+        if (ctx->copyin_pool) cp.run(items, in);
+        else
+            for (uint64_t k = 0; k < items; ++k) in(k);
         e->received = given;
     } else {  // TooManyOriginalShards at shard N, after N were added (lib.rs:281-284)
         for (uint64_t i = 0; i < given && st == RS_OK; ++i) st = rs_encoder_add_original_shard(e, original[i], S, err);
     }
+    // (measured and dropped, profiles/r06j, r06l: the recovery rows straight into the
+    // caller's pageable buffer, 149-154 against 117-120 us; the rows back in 2 / 4 / 8
+    // pieces with the copy-out of each overlapping the next, 111-123 / 144-163 / 197-212
+    // against 107-109 us -- every extra copy and event wait costs more than it hides)
     if (st == RS_OK) st = rs_encoder_encode(e, err);
     if (st == RS_OK && recovery_out)
         cp.run((M + per - 1) / per, [&](uint64_t k) {
@@ -2470,15 +2482,20 @@ rs_status rs_decode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const u
         st = dec_add(d, false, recovery_index[i], nullptr, S, err, false);
     CopyPool &cp = ctx->copies();
     const uint64_t per = copy_rows_per_item(S), given = original_given + recovery_given;
-    if (st == RS_OK)
-        cp.run((given + per - 1) / per, [&](uint64_t k) {
-            for (uint64_t j = k * per; j < std::min(given, k * per + per); ++j) {
-                const bool o = j < original_given;
-                const uint64_t i = o ? j : j - original_given;
-                insert_row((o ? d->h_orig : d->h_rec).p + (o ? original_index : recovery_index)[i] * d->row,
-                           (o ? original : recovery)[i], S);
-            }
-        });
+    auto in = [&](uint64_t k) {
+        for (uint64_t j = k * per; j < std::min(given, k * per + per); ++j) {
+            const bool o = j < original_given;
+            const uint64_t i = o ? j : j - original_given;
+            insert_row((o ? d->h_orig : d->h_rec).p + (o ? original_index : recovery_index)[i] * d->row,
+                       (o ? original : recovery)[i], S);
+        }
+    };
+    if (st == RS_OK) {
+        const uint64_t items = (given + per - 1) / per;
+        if (ctx->copyin_pool) cp.run(items, in);
+        else
+            for (uint64_t k = 0; k < items; ++k) in(k);
+    }
     if (st == RS_OK) st = rs_decoder_decode(d, err);
     if (st == RS_OK && d->decoded) {
         std::vector<uint64_t> miss;

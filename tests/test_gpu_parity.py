@@ -1641,7 +1641,8 @@ def _ptrs(rows):
     return (ctypes.c_void_p * max(1, len(rows)))(*[r.ctypes.data for r in rows])
 
 
-@pytest.mark.parametrize("N,M,S", [(1024, 1024, 1024), (3, 5, 64), (300, 200, 130), (100, 1000, 256), (5000, 300, 64)])
+@pytest.mark.parametrize("N,M,S", [(1024, 1024, 1024), (3, 5, 64), (300, 200, 130), (100, 1000, 256), (5000, 300, 64),
+                                   (1000, 2000, 130)])
 def test_c_oneshot_matches_oracle(torch, rs, N, M, S):
     import ctypes
     lib = _c_oneshot(rs)
