@@ -2264,7 +2264,7 @@ rs_status rs_decoder_reset(rs_decoder *d, uint64_t N, uint64_t M, uint64_t S, rs
 // copies the shards into the staging afterwards, in parallel
 static rs_status dec_add(rs_decoder *d, bool orig, uint64_t index, const uint8_t *shard, uint64_t len, rs_error *err,
                          bool copy = true) {
-    if (!d || (copy && !shard && len)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
+    if (!d || (!shard && len)) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     decoder_drop_result(d);
     const uint64_t count = orig ? d->N : d->M;
     std::vector<uint8_t> &present = orig ? d->orig_present : d->rec_present;
@@ -2415,13 +2415,18 @@ rs_status rs_encode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const u
         if (err) err->original_count = N, err->original_received_count = 0;
         return RS_ERR_TOO_FEW_ORIGINAL_SHARDS;
     }
+    if (!original) return set_err(err, RS_ERR_INVALID_ARGUMENT);
     (void)S;  // shard size is inferred from the first shard, as the reference does; S = its length
     rs_encoder *e = nullptr;
     rs_status st = rs_encoder_new_with_work(ctx, RS_RATE_DEFAULT, N, M, S, pool_take(ctx, ctx->enc_pool), &e, err);
     if (st != RS_OK) return st;
     CopyPool &cp = ctx->copies();
     const uint64_t per = copy_rows_per_item(S);
-    if (given <= N) {
+    // a null shard pointer takes the checked path (rs_encoder_add_original_shard's
+    // RS_ERR_INVALID_ARGUMENT at that shard)
+    bool all_shards = true;
+    for (uint64_t i = 0; all_shards && S && i < std::min(given, N); ++i) all_shards = original[i] != nullptr;
+    if (given <= N && all_shards) {
         // every shard is S bytes by this entry point's contract, so the per-shard checks
         // (encoder_work.rs:56-65) cannot fail: the shards go into the staging in parallel
         auto in = [&](uint64_t k) {
@@ -2433,7 +2438,7 @@ rs_status rs_encode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const u
         else
             for (uint64_t k = 0; k < items; ++k) in(k);
         e->received = given;
-    } else {  // TooManyOriginalShards at shard N, after N were added (lib.rs:281-284)
+    } else {  // TooManyOriginalShards at shard N, after N were added (lib.rs:281-284); null shards
         for (uint64_t i = 0; i < given && st == RS_OK; ++i) st = rs_encoder_add_original_shard(e, original[i], S, err);
     }
     // (measured and dropped, profiles/r06j, r06l: the recovery rows straight into the
@@ -2469,6 +2474,8 @@ rs_status rs_decode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const u
         if (err) err->original_count = N, err->original_received_count = original_given;
         return RS_ERR_NOT_ENOUGH_SHARDS;
     }
+    if ((original_given && (!original_index || !original)) || (recovery_given && (!recovery_index || !recovery)))
+        return set_err(err, RS_ERR_INVALID_ARGUMENT);
     rs_decoder *d = nullptr;
     rs_status st = rs_decoder_new_with_work(ctx, RS_RATE_DEFAULT, N, M, S, pool_take(ctx, ctx->dec_pool), &d, err);
     if (st != RS_OK) return st;
@@ -2477,9 +2484,9 @@ rs_status rs_decode(rs_context *ctx, uint64_t N, uint64_t M, uint64_t S, const u
     // indices are checked in the reference's order (decoder_work.rs:62-117) first,
     // then the shards go into the staging in parallel (CopyPool)
     for (uint64_t i = 0; i < original_given && st == RS_OK; ++i)
-        st = dec_add(d, true, original_index[i], nullptr, S, err, false);
+        st = dec_add(d, true, original_index[i], original[i], S, err, false);
     for (uint64_t i = 0; i < recovery_given && st == RS_OK; ++i)
-        st = dec_add(d, false, recovery_index[i], nullptr, S, err, false);
+        st = dec_add(d, false, recovery_index[i], recovery[i], S, err, false);
     CopyPool &cp = ctx->copies();
     const uint64_t per = copy_rows_per_item(S), given = original_given + recovery_given;
     auto in = [&](uint64_t k) {

@@ -1671,8 +1671,9 @@ def test_c_oneshot_matches_oracle(torch, rs, N, M, S):
     assert_rows_equal(rest[lost], orig[lost], "rs_decode")
     assert np.all(rest[have] == 0x33)
     # the reference's error order survives the checks-first / copies-after split
-    dup = np.concatenate([oidx[:2], oidx[:1]]).astype(np.uint64)
-    assert lib.rs_decode(ctx, N, M, S, dup.ctypes.data, _ptrs(orows[:3]), 3, ridx.ctypes.data, _ptrs(rrows),
+    dup = np.array([oidx[0], oidx[min(1, len(oidx) - 1)], oidx[0]], np.uint64)  # (a duplicate by the 3rd at the latest)
+    dup_rows = [orows[0], orows[min(1, len(orows) - 1)], orows[0]]
+    assert lib.rs_decode(ctx, N, M, S, dup.ctypes.data, _ptrs(dup_rows), 3, ridx.ctypes.data, _ptrs(rrows),
                          len(rrows), rest.ctypes.data, mask.ctypes.data, ctypes.byref(err)) == 2  # duplicate original
     bad = np.array([N], np.uint64)
     assert lib.rs_decode(ctx, N, M, S, bad.ctypes.data, _ptrs(orows[:1]), 1, ridx.ctypes.data, _ptrs(rrows),
@@ -1682,3 +1683,13 @@ def test_c_oneshot_matches_oracle(torch, rs, N, M, S):
     assert lib.rs_encode(ctx, N, M, S, _ptrs(extra), N + 1, out.ctypes.data, ctypes.byref(err)) == 9  # too many
     assert lib.rs_encode(ctx, N, M, S, _ptrs(rows), N - 1 if N > 1 else 0, out.ctypes.data,
                          ctypes.byref(err)) == 8  # too few
+    nul = _ptrs(rows)
+    nul[N // 2] = None  # a null shard pointer: the checked path's invalid-argument code
+    assert lib.rs_encode(ctx, N, M, S, nul, N, out.ctypes.data, ctypes.byref(err)) == 101
+    onul = _ptrs(orows)
+    onul[0] = None
+    assert lib.rs_decode(ctx, N, M, S, oidx.ctypes.data, onul, len(orows), ridx.ctypes.data, _ptrs(rrows),
+                         len(rrows), rest.ctypes.data, mask.ctypes.data, ctypes.byref(err)) == 101
+    # and the context still encodes afterwards
+    assert lib.rs_encode(ctx, N, M, S, _ptrs(rows), N, out.ctypes.data, ctypes.byref(err)) == 0
+    assert_rows_equal(out, want, "rs_encode after errors")
