@@ -1445,6 +1445,127 @@ __device__ __forceinline__ void col_walsh(uint32_t (&x)[2], uint32_t *buf) {
     x[1] = walsh_fold(x[1]);
 }
 
+// eval_poly with two LDS remaps instead of four exchange rounds (L = 10, 3 wave bits;
+// RS_MONO_EVAL_REMAP=0: col_walsh's rounds everywhere, 2: also L = 11).  Walsh-Hadamard layers on
+// different bits commute, and only the final layout matters (rows 2t, 2t + 1), so:
+//   layout O (as col_walsh): point p = k | lane << 1 | wave << 7
+//   layout T: bits 7..L-1 on lane bits 0..WB-1 (WB = L - 7 wave bits), bits 1..6-WB on
+//             lane bits WB..5, bits 7-WB..6 on the wave bits, bit 0 = k
+// transform 1: bits 0..6 in O, remap O -> T, bits 7..L-1; x lw_fold (in T); transform 2:
+// bits 7..L-1, 0, 1..6-WB in T, remap T -> O, bits 7-WB..6.  The two remaps use the two
+// buffers the rounds used, the last one `buf` (see col_eval_poly on what is written next).
+#ifndef RS_MONO_EVAL_REMAP
+#define RS_MONO_EVAL_REMAP 1
+#endif
+// Measured (profiles/r06o/eval_remap_ab.txt, µs per launch, 3 alternating rounds, same output):
+// 2^10 work rows 1 % / 100 % 8.84-8.91 / 8.59-8.61 -> 8.68-8.76 / 8.37-8.44; 2^11 1 %
+// 12.38-12.54 -> 12.24-12.50 but 100 % 12.24-12.35 -> 12.40-12.54.  So 2^10 only
+// (RS_MONO_EVAL_REMAP=2: 2^11 too).
+template <int L>
+constexpr bool kEvalRemap = (RS_MONO_EVAL_REMAP != 0 && L == 10) || (RS_MONO_EVAL_REMAP == 2 && L == 11);
+// layout T: the u32 index (point / 2) of a thread's point pair
+template <int L>
+__device__ __forceinline__ uint32_t eval_t_pair(uint32_t lane, uint32_t wave) {
+    constexpr int WB = L - 7;
+    return (lane >> WB) | (wave << (6 - WB)) | ((lane & ((1u << WB) - 1u)) << 6);
+}
+// LDS slot of a point pair q (< 2^(L-1)): its bits 6.. (the wave in layout O, the lane
+// bits 0..WB-1 in layout T) XORed into bits 6-WB..5, so the 64 lanes of a wave hit 64
+// different low slot bits in both layouts (uint2 slots: conflict-free ds_*_b64)
+template <int L>
+__device__ __forceinline__ uint32_t eval_swz(uint32_t q) {
+    constexpr int WB = L - 7;
+    return q ^ ((q >> 6) << (6 - WB));
+}
+template <int J, int K>
+__device__ __forceinline__ void walsh_lane(uint32_t (&x)[2], uint32_t lane) {
+    const uint32_t m = (lane & (1u << J)) ? ~0u : 0u;
+    const uint32_t c = m & kWalshM1<K>;
+    static_for<0, 2>([&](auto kc) {
+        constexpr int q = decltype(kc)::value;
+        const uint32_t y = lane_xor<J>(x[q], lane);
+        x[q] = y + (x[q] ^ m) + c;
+    });
+}
+template <int K>
+__device__ __forceinline__ void walsh_reg(uint32_t (&x)[2]) {
+    const uint32_t p = x[0], q = x[1];
+    x[0] = p + q;
+    x[1] = p + ~q + kWalshM1<K>;
+}
+// O -> T (to_t) or T -> O through uint2 slots of buf (2^L words)
+template <int L, bool TO_T>
+__device__ __forceinline__ void eval_remap(uint32_t (&x)[2], uint32_t *buf, uint32_t lane, uint32_t wave) {
+    uint2 *b = reinterpret_cast<uint2 *>(buf);
+    const uint32_t o = threadIdx.x, t = eval_t_pair<L>(lane, wave);
+    b[eval_swz<L>(TO_T ? o : t)] = uint2{x[0], x[1]};
+    __syncthreads();
+    const uint2 v = b[eval_swz<L>(TO_T ? t : o)];
+    x[0] = v.x;
+    x[1] = v.y;
+}
+template <int L>
+__device__ __forceinline__ void col_eval_poly_remap(const MonoCore &A, uint32_t ebits, uint32_t rbits,
+                                                   const uint32_t &lwv, uint32_t *buf, uint32_t *rinfo) {
+    constexpr int WB = L - 7;
+    static_assert(WB >= 1 && WB <= 4, "eval_poly remap: 1 to 4 wave bits");
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t i0 = 2 * threadIdx.x;
+    uint32_t x[2];
+    static_for<0, 2>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const uint32_t e = (ebits >> k) & 1u, i = i0 + k;
+        x[k] = A.low_rate ? (i < A.end ? (e ? 0u : 65534u) : 0u) : e;  // (rate_low.rs:196)
+    });
+    // transform 1: bits 0..6 (layout O), then bits 7..L-1 (layout T)
+    walsh_reg<0>(x);
+    static_for<0, 6>([&](auto jc) {
+        constexpr int J = decltype(jc)::value;
+        walsh_lane<J, J + 1>(x, lane);
+    });
+    RS_MSTAMP(19);
+    eval_remap<L, true>(x, buf + (1u << L), lane, wave);
+    static_for<0, WB>([&](auto jc) {
+        constexpr int J = decltype(jc)::value;
+        walsh_lane<J, 7 + J>(x, lane);
+    });
+    x[0] = walsh_fold(x[0]);
+    x[1] = walsh_fold(x[1]);
+    RS_MSTAMP(14);
+    // x lw_fold of the thread's layout-T points (lwv: loaded for that pair, mono_body)
+    const uint32_t lw[2] = {lwv & 0xFFFFu, lwv >> 16};
+    const bool p0 = lane == 0 && wave == 0;  // layout T's point 0
+    static_for<0, 2>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const uint32_t p = x[k] * lw[k];
+        uint32_t f = ev_add(p & 0xFFFFu, p >> 16);
+        if (k == 0 && A.low_rate && p0) f = ev_add(f, A.lw0);
+        x[k] = f;
+    });
+    // transform 2: bits 7..L-1, 0, 1..6-WB (layout T), then bits 7-WB..6 (layout O)
+    static_for<0, WB>([&](auto jc) {
+        constexpr int J = decltype(jc)::value;
+        walsh_lane<J, J>(x, lane);
+    });
+    walsh_reg<WB>(x);
+    static_for<WB, 6>([&](auto jc) {
+        constexpr int J = decltype(jc)::value;
+        walsh_lane<J, J + 1>(x, lane);
+    });
+    RS_MSTAMP(20);
+    eval_remap<L, false>(x, buf, lane, wave);
+    static_for<6 - WB, 6>([&](auto jc) {
+        constexpr int J = decltype(jc)::value;
+        walsh_lane<J, J + WB + 1>(x, lane);
+    });
+    x[0] = walsh_fold(x[0]);
+    x[1] = walsh_fold(x[1]);
+    // rinfo of rows 2t, 2t + 1 (layout O), read next by this wave (see col_eval_poly)
+    reinterpret_cast<uint2 *>(rinfo)[threadIdx.x] =
+        uint2{x[0] | ((rbits & 1u) ? 0u : 0x10000u), x[1] | ((rbits & 2u) ? 0u : 0x10000u)};
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 // rinfo[r] = log factor | (received ? 0 : 0x10000) for the 2^L work rows.
 // ebits / rbits: this thread's erased / received bits (bits 0, 1 = rows 2t,
 // 2t+1); lwv: lw_fold of those rows (two 16-bit values), an ordinary load the
@@ -1455,6 +1576,10 @@ __device__ __forceinline__ void col_walsh(uint32_t (&x)[2], uint32_t *buf) {
 template <int L>
 __device__ __forceinline__ void col_eval_poly(const MonoCore &A, uint32_t ebits, uint32_t rbits, const uint32_t &lwv,
                                               uint32_t *buf, uint32_t *rinfo) {
+    if constexpr (kEvalRemap<L>) {
+        col_eval_poly_remap<L>(A, ebits, rbits, lwv, buf, rinfo);
+        return;
+    }
     const uint32_t i0 = 2 * threadIdx.x;
     uint32_t x[2];
     static_for<0, 2>([&](auto kc) {
@@ -1757,7 +1882,9 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 rbits = (g == 0 ? r0 : g == 1 ? r1 : g == 2 ? r2 : r3) >> sh;
                 // lw_fold of rows 2t, 2t + 1 as one dword (the context keeps every
                 // 2^u-entry segment 4-byte aligned, rs_codec.cpp rs_context_create)
-                lwv = reinterpret_cast<const uint32_t *>(A.lw_fold)[threadIdx.x];
+                // (RS_MONO_EVAL_REMAP: the pair of the thread's layout-T points, col_eval_poly_remap)
+                lwv = reinterpret_cast<const uint32_t *>(A.lw_fold)[kEvalRemap<L> ? eval_t_pair<L>(lane, wave)
+                                                                                 : threadIdx.x];
                 asm volatile("" ::: "memory");  // issued first, ahead of every other load
             }
             // Decodes: a wave whose phase-1 rows hold no received row (!live) loads
