@@ -449,6 +449,24 @@ struct LdsTabs {
     const uint32_t *priv, *shared, *img_i, *img_f;
     template <int, int, typename S, int I, int PH>
     __device__ __forceinline__ void get(int x, uint32_t row, uint32_t (&t)[Fmt<E>::kTW]) const {
+#ifdef RS_MONO_FAKE_TABS  // tools/mono_probe.hip: tables without LDS traffic
+        const uint32_t *fb = tab<0, 0, S, I, PH>(x, row);
+        for (int q = 0; q < G::TW; ++q) t[q] = q + uint32_t(reinterpret_cast<uintptr_t>(fb));
+        return;
+#endif
+        read(tab<0, 0, S, I, PH>(x, row), t);
+    }
+    static __device__ __forceinline__ void read(const uint32_t *tb, uint32_t (&t)[Fmt<E>::kTW]) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(tb);
+#pragma unroll
+        for (int q = 0; q < int(G::PC); ++q) {
+            const uint4 v = p[q];
+            t[4 * q] = v.x, t[4 * q + 1] = v.y, t[4 * q + 2] = v.z, t[4 * q + 3] = v.w;
+        }
+    }
+    // the LDS slot of the table of row `row`'s butterfly group at layer x
+    template <int, int, typename S, int I, int PH>
+    __device__ __forceinline__ const uint32_t *tab(int x, uint32_t row) const {
         uint32_t slot;
         const uint32_t *base;
         if constexpr ((PH == 1 || PH == 3) && G::B0 == 1 && S::v.ops[I].bit == 0) {
@@ -464,18 +482,10 @@ struct LdsTabs {
             slot = G::kShI + (G::n >> G::FLO) - (G::n >> x) + G::sg(row >> (x + 1));
             base = shared;
         }
-#ifdef RS_MONO_FAKE_TABS  // tools/mono_probe.hip: tables without LDS traffic
-        for (int q = 0; q < G::TW; ++q) t[q] = slot * 0x01010101u + q + uint32_t(reinterpret_cast<uintptr_t>(base));
-        return;
-#endif
-        const uint4 *p = reinterpret_cast<const uint4 *>(base) + slot * G::SPC;
-#pragma unroll
-        for (int q = 0; q < int(G::PC); ++q) {
-            const uint4 v = p[q];
-            t[4 * q] = v.x, t[4 * q + 1] = v.y, t[4 * q + 2] = v.z, t[4 * q + 3] = v.w;
-        }
+        return base + slot * G::SW;
     }
 };
+
 
 // Phase of op I of a sequence: 1 = IFFT in-wave low bits, 2 = IFFT top bits,
 // 4 = FFT top bits (shared region, FFT part), 3 = FFT in-wave low bits.
@@ -579,6 +589,53 @@ constexpr int layer_at(const Seq &s, int k) {
     return s.count;
 }
 constexpr int num_layers(const Seq &s) { return layer_ordinal(s, s.count); }
+
+// The same tables with every layer's slot address of the lane computed once, up
+// front (one pair per lane, LR = 1), and held in VGPRs: the layers then issue
+// their ds_read_b128s straight from a register instead of 3-5 VALU of slot
+// arithmetic each, and the arithmetic runs while the prologue's loads are in
+// flight (RS_MONO_PRE_ADDR=1; 2^11-row kernels keep LdsTabs: at 4 waves per SIMD
+// their 20 more VGPRs would not fit).  NI / NF: whether the IFFT / FFT runs.
+// Measured slower, so off (profiles/r06q/pre_addr_ab.txt, same output bytes and the
+// GPU suite green with it on): the per-layer arithmetic shares terms between the
+// layers of a placement, the pinned addresses cannot, and the headline encode issues
+// 2.10 M instead of 2.00 M VALU per launch (8.94 -> 9.08-9.10 us, 2^10-row decode
+// at 1 % 9.72-9.75 -> 10.04-10.13 us).
+#ifndef RS_MONO_PRE_ADDR
+#define RS_MONO_PRE_ADDR 0
+#endif
+template <int L, int LR, int SPLIT, int E, bool NI, bool NF>
+struct LdsTabsPre {
+    using T = LdsTabs<L, LR, SPLIT, E>;
+    using SI = SeqOf<L, LR, false, SPLIT>;
+    using SF = SeqOf<L, LR, true, SPLIT>;
+    static_assert(LR == 1, "one table per layer and lane");
+    static constexpr int KI = NI ? num_layers(SI::v) : 1, KF = NF ? num_layers(SF::v) : 1;
+    const uint32_t *lds0;
+    uint32_t ai[KI], af[KF];  // byte offsets from lds0, by layer ordinal
+    template <typename S, bool FFT, int K>
+    __device__ __forceinline__ void fill(const T &ts, uint32_t lane, uint32_t wave, uint32_t (&a)[K]) {
+        static_for<0, K>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int I = layer_at(S::v, k);
+            a[k] = uint32_t(reinterpret_cast<const char *>(ts.template tab<0, 0, S, I, phase_of<S, FFT, I>()>(
+                                S::v.ops[I].bit, lane_rows<S, I>(lane, wave))) -
+                            reinterpret_cast<const char *>(lds0));
+            asm volatile("" : "+v"(a[k]));  // computed here, kept in a VGPR
+        });
+    }
+    __device__ __forceinline__ LdsTabsPre(const T &ts, const uint32_t *lds, uint32_t lane, uint32_t wave) : lds0(lds) {
+        if constexpr (NI) fill<SI, false>(ts, lane, wave, ai);
+        if constexpr (NF) fill<SF, true>(ts, lane, wave, af);
+    }
+    template <int, int, typename S, int I, int PH>
+    __device__ __forceinline__ void get(int, uint32_t, uint32_t (&t)[Fmt<E>::kTW]) const {
+        constexpr bool F = std::is_same<S, SF>::value;
+        static_assert(F ? NF : NI, "the transform's addresses were not computed");
+        constexpr int k = layer_ordinal(S::v, I);
+        T::read(reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds0) + (F ? af[k] : ai[k])), t);
+    }
+};
 
 #ifndef RS_MONO_PF
 #define RS_MONO_PF 3
@@ -2040,6 +2097,14 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
             }
             if constexpr (HSC) scale_issue<L, LR, PK, E>(A, A.rowinfo + (hh << L), st, lane, wave, true);
             RS_MSTAMP(13);
+            // the layers' table source (LdsTabsPre: slot addresses computed here, while
+            // the loads above are in flight)
+            const LdsTabs<L, LR, PK, E> ts_lds{priv, shared, img_i, img_f};
+            constexpr bool kPreAddr = RS_MONO_PRE_ADDR && LR == 1 && L <= 10;
+            const auto ts = [&]() {
+                if constexpr (kPreAddr) return LdsTabsPre<L, LR, PK, E, !HALF_F, !HALF_I>(ts_lds, lds, lane, wave);
+                else return ts_lds;
+            }();
             auto write1 = [&]() {
 #ifndef RS_MONO_SKIP_STAGE
                 static_for<0, KP1>([&](auto kc) {
@@ -2087,7 +2152,6 @@ __device__ __forceinline__ void mono_body(const MonoArgT<MODE, STAGED> &K) {
                 finish_col<L, LR, DEC || HSC>(w, okm, &st, c, lane, io);
             }
             RS_MSTAMP(1);
-            const LdsTabs<L, LR, PK, E> ts{priv, shared, img_i, img_f};
             // phase-3 tables: requested when phase 1 ends, written over this wave's
             // phase-1 tables when phase 2 ends
             uint4 v3[KP3];
