@@ -1431,6 +1431,18 @@ void decode_dev(rs_context *ctx, Workspace &ws, bool high, const Geom &g, uint64
     T.fd_mode = 1;
     T.work_out = U;
     T.blk_masks = top_masks ? 1 : 0;
+    // its butterflies pruned by block (rs_kernels.hip Prune): the IFFT skips groups of
+    // zero-input blocks, the FFT groups that feed no block with restored rows
+    // (RS_MI355X_BFLY_PRUNE=0: off, A/B)
+    static const bool bfly_prune = !getenv("RS_MI355X_BFLY_PRUNE") || getenv("RS_MI355X_BFLY_PRUNE")[0] != '0';
+    if (bfly_prune && masks && lv.K[lv.m - 1] <= 6) {
+        const std::vector<uint64_t> need = count_per_block(st, nd, G, out_map.row_begin, out_map.row_end, 1);
+        T.bfly_prune = 1;
+        T.zin_local = top_masks ? A.zero_in[0] : 0;
+        T.need_local = 0;
+        for (uint32_t b = 0; b < need.size(); ++b)
+            if (need[b]) T.need_local |= 1ull << b;
+    }
     run_level(T, lv, lv.m - 1, rs::kIfft | rs::kFft, nd, s);
     A.blk_masks = skips ? 1 : 0;  // the passes below the top read X[k]: zero blocks load as zero
     A.blk_uniform = 1;

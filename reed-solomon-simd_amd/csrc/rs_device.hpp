@@ -159,6 +159,16 @@ struct PassArgs {
     uint32_t fused_eval = 0, ev_low_rate = 0, ev_end = 0, ev_lw0 = 0;
     const uint16_t *ev_lw_fold = nullptr;      // lw_fold for 2^K points
     uint32_t ev_erased[2] = {0, 0}, ev_received[2] = {0, 0};
+
+    // ---- the fused top pass of a multi-pass decode (bfly_prune = 1, K <= 6): its
+    // local row j lies in block j (the top level's rows are the 2^K blocks of
+    // 2^a rows).  zin_local bit j: block j's IFFT input is zero (zero_in);
+    // need_local bit j: block j holds restored rows.  The IFFT skips the butterfly
+    // groups whose 2^(b+1) rows are all zero (their outputs stay zero), the FFT
+    // those that feed no needed block (their rows are never read: the FFT passes
+    // below read only the needed blocks' rows)
+    uint32_t bfly_prune = 0;
+    uint64_t zin_local = 0, need_local = ~0ull;
 };
 constexpr uint32_t kPassEvalRows = 64;
 

@@ -25,6 +25,12 @@ namespace rs {
 namespace {
 
 
+// Block pruning of the decode's fused top pass (PassArgs::bfly_prune; 0: the
+// variant without it, for A/B)
+#ifndef RS_PASS_BFLY_PRUNE
+#define RS_PASS_BFLY_PRUNE 1
+#endif
+
 // -------------------------------------------------------------------------
 // Pass kernel.
 //   K   : log2 rows per set (the butterfly layers this pass runs)
@@ -498,18 +504,36 @@ __device__ __forceinline__ void store_rows(const PassArgs &A, const Ctx &c, uint
     });
 }
 
+// Block pruning of the decode's fused top pass (PassArgs::bfly_prune): local
+// rows are blocks, zin / need the masks of zero-input / needed blocks.  The
+// butterfly group of local row j at layer B covers the 2^(B+1) rows that share
+// j's bits above B; an IFFT group is skipped when all of them are zero, an FFT
+// group when none of them is needed (K <= 6: the masks are 64-bit).
+struct Prune {
+    uint64_t zin = 0, need = ~0ull;
+};
+template <bool IFFT, int B>
+__device__ __forceinline__ bool group_live(const Prune &pr, uint32_t j) {
+    constexpr uint64_t blk = B + 1 >= 6 ? ~0ull : (1ull << (1u << (B + 1))) - 1ull;
+    const uint32_t base = j & ~((2u << B) - 1u);
+    return IFFT ? ((pr.zin >> base) & blk) != blk : ((pr.need >> base) & blk) != 0;
+}
+
 // One butterfly layer on local bit B (global bit a + B), rows in phase PH.
-template <int K, int LR, int SPL, int PH, int B, bool IFFT>
+template <int K, int LR, int SPL, int PH, int B, bool IFFT, bool PRUNE = false>
 __device__ __forceinline__ void layer(const Ctx &c, const uint32_t *tab, uint32_t (&lo)[1 << LR],
-                                      uint32_t (&hi)[1 << LR]) {
+                                      uint32_t (&hi)[1 << LR], const Prune &pr = Prune{}) {
     using P = Pass<K, LR, SPL>;
     constexpr int RB = B - P::start(PH);  // register bit
     static_assert(RB >= 0 && RB < LR, "bit not resident in this phase");
+    static_assert(!PRUNE || (K <= 6 && P::kUniform), "block pruning: wave-uniform row groups, 64-bit masks");
     // Butterfly groups held by the lane: register index bits above RB.  One
     // 20-word table per group, read from LDS once for its 2^RB butterflies.
     uint32_t dep = 0;
     static_for<0, (P::R >> (RB + 1))>([&](auto gc) {
         constexpr int i0 = decltype(gc)::value << (RB + 1);
+        if constexpr (PRUNE)
+            if (!group_live<IFFT, B>(pr, P::template lrow<PH>(c.g, i0))) return;  // (uniform)
         uint32_t off = tw_slot<K>(B, P::template lrow<PH>(c.g, i0)) * 20u;
         if constexpr (P::kSerial) {  // one table in flight
             if constexpr (P::kUniform) asm volatile("" : "+s"(off) : "v"(dep));
@@ -695,9 +719,11 @@ __device__ __forceinline__ void apply_layer(const LayerTabs<LR> &T, uint32_t (&l
 // while layer n runs, so the LDS latency hides behind the butterflies and
 // the phase exchanges; wide shapes read one table at a time (registers).
 // ZT: layer K-1 has a zero twiddle (kZeroI / kZeroF): no table, no multiply.
-template <int K, int LR, int SPL, bool IFFT, bool ZT = false>
+// PRUNE: block pruning of the decode's fused top pass (Prune, serial wide shapes).
+template <int K, int LR, int SPL, bool IFFT, bool ZT = false, bool PRUNE = false>
 __device__ __forceinline__ void transform(const Ctx &c, uint32_t *plane, const uint32_t *tab,
-                                          uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR]) {
+                                          uint32_t (&lo)[1 << LR], uint32_t (&hi)[1 << LR],
+                                          const Prune &pr = Prune{}) {
     using P = Pass<K, LR, SPL>;
 #ifdef RS_PROBE_SKIP_XFORM  // tools/pass_probe.hip: time a pass without its layers
     return;
@@ -711,7 +737,7 @@ __device__ __forceinline__ void transform(const Ctx &c, uint32_t *plane, const u
             if constexpr (n > 0 && P::phase_of(prev) != ph)
                 exchange<K, LR, SPL, P::phase_of(prev), ph>(c, plane, lo, hi);
             if constexpr (ZT && b == K - 1) xor_layer<K, LR, SPL, ph, b>(lo, hi);
-            else layer<K, LR, SPL, ph, b, IFFT>(c, tab, lo, hi);
+            else layer<K, LR, SPL, ph, b, IFFT, PRUNE>(c, tab, lo, hi, pr);
         });
     } else {
         LayerTabs<LR> T[2];
@@ -825,6 +851,12 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
 
     const Ctx c = make_ctx<K, LR, SPL>(A, bx);
     const uint32_t gchunk = by;
+    // the decode's fused top pass: block pruning of its butterflies (PassArgs::bfly_prune)
+    constexpr bool PRUNE = RS_PASS_BFLY_PRUNE && FD && DO_IFFT && DO_FFT && !REVEAL && !MULTI_IN && !MULTI_OUT &&
+                           K <= 6 && P::kSerial && P::kUniform;
+    Prune pr;
+    if constexpr (PRUNE)
+        if (A.bfly_prune) pr = Prune{A.zin_local, A.need_local};
 
     uint32_t lo[P::R], hi[P::R];
     uint32_t xl[XOR_IN ? P::R : 1], xh[XOR_IN ? P::R : 1];
@@ -853,7 +885,7 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
     if constexpr (SCALE) scale_rows<K, LR, SPL, 0>(c, tabS, lo, hi);
 
     if constexpr (DO_IFFT) {
-        transform<K, LR, SPL, true, ZI>(c, plane, tabI, lo, hi);
+        transform<K, LR, SPL, true, ZI, PRUNE>(c, plane, tabI, lo, hi, pr);
         if constexpr (MULTI_IN) {
             for (uint32_t ci = 1; ci < A.in_chunks; ++ci) {
                 const uint32_t chunk = gchunk + ci;
@@ -881,7 +913,7 @@ __device__ __forceinline__ void pass_body(const PassArgs &A, uint32_t bx, uint32
     if constexpr (XOR_IN) static_for<0, P::R>([&](auto ic) { lo[ic] ^= xl[ic]; hi[ic] ^= xh[ic]; });
 
     if constexpr (DO_FFT && !MULTI_OUT) {
-        transform<K, LR, SPL, false, ZF>(c, plane, tabF, lo, hi);
+        transform<K, LR, SPL, false, ZF, PRUNE>(c, plane, tabF, lo, hi, pr);
         store_rows<K, LR, SPL, 0, REVEAL>(A, c, gchunk, tabV, rinfo, lo, hi);
     } else if constexpr (DO_FFT) {
         for (uint32_t co = 0; co < A.out_chunks; ++co) {
